@@ -1,0 +1,272 @@
+#!/usr/bin/env python3
+"""bench.py — Mrays/s + ms/frame of the MI355X trace/shade path (BASELINE.json metric).
+
+A "step" is one pass of the hot path over one batch of synthetic input: every rank
+renders one full frame of the configured scene (default c2: 1920x1080, 8 spheres +
+4 walls, reflection depth 4) into HBM through the C-ABI (rt_render_device), the scene
+already resident on the device.  With N ranks the batch is N frames of a camera
+fly-through (rank r renders frame r: the camera moved r steps forward the way
+Camera::forward moves it, scene.cpp:121) — frames are independent units, sharded with
+no data-path collective, so `scaling` is "weak".  `--mode tiled` instead splits ONE
+frame into row bands across ranks and gathers them to rank 0 (RCCL), the strong-scaling
+layout of BASELINE config 4.
+
+Rays = segments = closest-hit queries (primary + reflection), counted exactly by the
+kernel in an untimed census launch.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2] [--precision mixed]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "ray-tracer-from-scratch_amd"))
+
+from rtamd import capi, scenes  # noqa: E402
+
+METRIC = "Mrays/sec + ms/frame at 1920×1080 depth=4; 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+VALU_PEAK_TFLOPS = {"f32": 157.3, "mixed": 157.3, "f64": 78.6}   # vector peaks (spec)
+
+
+def flop_per_segment(n_sph: int, n_wall: int) -> int:
+    """SURVEY §8d convention: F_seg = 30*N_sphere + 38*N_wall + 60 (FMA = 2)."""
+    return 30 * n_sph + 38 * n_wall + 60
+
+
+def scene_bytes(n_sph: int, n_wall: int, n_prim: int) -> int:
+    return 64 * n_sph + 176 * n_wall + 64 * n_prim   # DevSphere / DevWall / DevMat records
+
+
+def cpu_baseline(cfg, prims, cam, depth, flags, budget_s: float):
+    """The oracle's OpenMP restatement (the 'OpenMP CPU path') on this host's cores, on a
+    bounded sample of the same frame: a centred band of rows sized to ~budget_s."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as orc_mod   # test infrastructure: the timed CPU baseline leg only
+    orc = orc_mod.Oracle()
+    cores = max(1, min(16, len(os.sched_getaffinity(0))))
+    H = cam.height
+    probe = min(H, 16)
+    r0 = max(0, H // 2 - probe // 2)
+    t = time.perf_counter()
+    orc.render(prims, cam, depth, flags, row0=r0, nrows=probe, nthreads=cores, want64=False)
+    per_row = max(1e-6, (time.perf_counter() - t) / probe)
+    rows = int(min(H, max(probe, budget_s / per_row)))
+    r0 = max(0, H // 2 - rows // 2)
+    t = time.perf_counter()
+    _, _, segs = orc.render(prims, cam, depth, flags, row0=r0, nrows=rows, nthreads=cores,
+                            want64=False)
+    dt = time.perf_counter() - t
+    return {"value": round(segs / dt / 1e6, 3), "unit": "Mrays/s", "cores": cores, "kind": "port",
+            "sample": f"rows {r0}..{r0 + rows - 1} of the same {cam.width}x{H} frame "
+                      f"({rows * cam.width} px, {segs} segments, {dt:.2f} s), fp64 oracle "
+                      f"restatement, OpenMP schedule(dynamic,1) over rows",
+            "ms_per_frame_extrapolated": round(dt / rows * H * 1e3, 1)}
+
+
+def load_traffic(path: str, workload: str, precision: str):
+    """Per-launch HBM bytes measured by rocprofv3 --pmc (profiles/)."""
+    try:
+        with open(path) as fh:
+            d = json.load(fh)
+        e = d.get(workload, {}).get(precision)
+        return None if e is None else float(e["hbm_bytes_per_launch"])
+    except (OSError, ValueError, KeyError, TypeError):
+        return None
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawTextHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="c2", choices=sorted(scenes.CONFIGS))
+    ap.add_argument("--precision", default="mixed", choices=sorted(capi.PRECISIONS))
+    ap.add_argument("--mode", default="frames", choices=["frames", "tiled"])
+    ap.add_argument("--sun", action="store_true", help="build-defined sun term (off = parity)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    cfg = scenes.CONFIGS[args.config]
+    sc = cfg.scene()
+    prims = scenes.to_prims(sc)
+    n_sph = sum(1 for o in sc if o.kind == capi.RT_PRIM_SPHERE)
+    n_wall = len(sc) - n_sph
+    prec = capi.PRECISIONS[args.precision]
+    flags = capi.RT_FLAG_SUN if args.sun else 0
+    depth = cfg.depth
+
+    rend = capi.Renderer(local)
+    rend.set_scene(prims)
+    cam = capi.camera_init(**scenes.camera_args(cfg.width, cfg.height))
+    W, H = cam.width, cam.height
+    if args.mode == "frames":
+        # frame `rank` of a fly-through: Camera::forward moves position by
+        # forward_vec()*movement_speed = (1,0,0)*0.1 and never re-calls init().
+        cam.position[0] += 0.1 * rank
+        row0, nrows = 0, H
+    else:
+        row0, nrows = capi.band_rows(H, world, rank)
+    band_max = -(-H // world) if args.mode == "tiled" else H
+
+    stream = torch.cuda.current_stream(dev)
+    out = torch.empty((band_max, W, 3), dtype=torch.float32, device=dev)
+    segs_t = torch.zeros(1, dtype=torch.int64, device=dev)
+    frame = torch.empty((H, W, 3), dtype=torch.float32, device=dev) if (
+        args.mode == "tiled" and rank == 0) else None
+    gather_list = ([torch.empty_like(out) for _ in range(world)]
+                   if (args.mode == "tiled" and rank == 0 and world > 1) else None)
+
+    def launch(d_segs: int = 0):
+        rend.render_device(cam, depth, out.data_ptr(), prec, flags, capi.RT_OUT_RGB_F32,
+                           row0=row0, nrows=nrows, d_segments=d_segs, stream=stream.cuda_stream)
+
+    def step():
+        launch()
+        if args.mode == "tiled" and world > 1:
+            dist.gather(out, gather_list, dst=0)
+            if rank == 0:
+                for r, g in enumerate(gather_list):
+                    a, n = capi.band_rows(H, world, r)
+                    frame[a:a + n].copy_(g[:n])
+
+    # census: exact segment count of this rank's share (untimed)
+    launch(segs_t.data_ptr())
+    torch.cuda.synchronize(dev)
+    my_segs = int(segs_t.item())
+    tot = torch.tensor([my_segs], dtype=torch.int64, device=dev)
+    if world > 1:
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+    total_segs = int(tot.item())
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    torch.cuda.synchronize(dev)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    barrier()
+    t1 = time.perf_counter()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed_s = float(elapsed.item())
+    stream_ms = ev0.elapsed_time(ev1) / args.steps
+
+    # per-launch kernel time (HIP events around launches alone, same stream)
+    ek0 = torch.cuda.Event(enable_timing=True)
+    ek1 = torch.cuda.Event(enable_timing=True)
+    nk = max(10, args.steps)
+    ek0.record(stream)
+    for _ in range(nk):
+        launch()
+    ek1.record(stream)
+    torch.cuda.synchronize(dev)
+    kernel_ms = ek0.elapsed_time(ek1) / nk
+
+    result = None
+    if rank == 0:
+        ms_step = elapsed_s / args.steps * 1e3
+        value = total_segs * args.steps / elapsed_s / 1e6
+        frames_per_step = world if args.mode == "frames" else 1
+        px_step = W * H * frames_per_step
+        kernel_s = kernel_ms * 1e-3
+        out_bytes = nrows * W * 12
+        alg_bytes = out_bytes + scene_bytes(n_sph, n_wall, len(sc))
+        workload = f"{cfg.name}:{W}x{H}:d{depth}:s{n_sph}w{n_wall}"
+        traffic = load_traffic(args.traffic_json, workload, args.precision)
+        flops = my_segs * flop_per_segment(n_sph, n_wall)
+        valu_peak = VALU_PEAK_TFLOPS[args.precision]
+        result = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak" if args.mode == "frames" else "strong",
+            "vs_baseline": None,
+            "dtype": "f64" if args.precision in ("f64", "mixed") else "f32",
+            "data": "synthetic",
+            "config": {
+                "workload": workload,
+                "scene": cfg.description + (" + sun" if args.sun else ""),
+                "width": W, "height": H, "depth": depth,
+                "spheres": n_sph, "walls": n_wall,
+                "precision": args.precision,
+                "cull_dtype": "f32" if args.precision == "mixed" else None,
+                "frames_per_step": frames_per_step,
+                "segments_per_step": total_segs,
+                "segments_per_pixel": round(total_segs / px_step, 4),
+                "parallelism": (f"frame-sharded x{world}" if args.mode == "frames"
+                                else f"row-tiled x{world} + gather"),
+            },
+            "ms_per_frame": round(ms_step / frames_per_step if args.mode == "frames" else ms_step, 4),
+            "mpx_per_s": round(px_step * args.steps / elapsed_s / 1e6, 2),
+            "kernel_ms": round(kernel_ms, 4),
+            "stream_ms_per_step": round(stream_ms, 4),
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(alg_bytes / kernel_s / 1e9, 2),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(alg_bytes / kernel_s / 1e9 / HBM_PEAK_GBS, 5),
+                "traffic": traffic,
+                "algorithmic_bytes_per_launch": alg_bytes,
+                "note": "north_star-mandated HBM view; the kernel is FP VALU-bound, see roofline_valu",
+            },
+            "roofline_valu": {
+                "bound": "valu",
+                "achieved": round(flops / kernel_s / 1e12, 3),
+                "peak": valu_peak,
+                "unit": "TFLOP/s",
+                "frac": round(flops / kernel_s / 1e12 / valu_peak, 4),
+                "flop_per_launch": flops,
+                "convention": "SURVEY 8d: F_seg = 30*N_sphere + 38*N_wall + 60, FMA = 2",
+            },
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline and args.cpu_seconds > 0:
+            result["cpu_baseline"] = cpu_baseline(cfg, prims, cam, depth, flags, args.cpu_seconds)
+        print(json.dumps(result), flush=True)
+    rend.close()
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

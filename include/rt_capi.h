@@ -1,0 +1,167 @@
+/*
+ * rt_capi.h — the C-ABI drop-in boundary of the MI355X trace/shade path.
+ *
+ * The reference renders a frame with one C++ call,
+ *     void rt_scene(std::vector<vec3> u, const std::vector<std::unique_ptr<SceneGeometry>>& scene,
+ *                   const Camera& cam, std::vector<std::vector<RGB>>& frame_buffer);
+ * (/root/reference/main.cpp:124-139), which walks every pixel through
+ * recursive_ray_tracing (main.cpp:89-119) -> find_closest_hit (main.cpp:67-84) ->
+ * the virtual SceneGeometry::intersect plugin (scene.h:57; Sphere::intersect
+ * scene.cpp:40-78, Wall::intersect scene.cpp:4-35).
+ *
+ * This header is what a host program binds instead: plain C, plain pointers and
+ * sizes, no C++ or torch types.  The C++ API mirror (include/rt/scene.h) flattens its
+ * SceneGeometry objects into rt_prim records and calls these entry points; a cgo /
+ * ctypes / N-API binding binds them directly.
+ *
+ * Conventions (the reference has no error returns; .at() throws — main.cpp:136):
+ *   - every entry point returns int status, RT_OK == 0; rt_strerror() names it;
+ *   - no exception crosses the boundary;
+ *   - a ctx is used by one host thread at a time; calls on a ctx are serialised;
+ *   - the caller owns every buffer passed in; the ctx owns its device copies.
+ */
+#ifndef RT_CAPI_H
+#define RT_CAPI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_CAPI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------- */
+enum rt_status {
+    RT_OK = 0,
+    RT_ERR_INVALID_ARG = 1,   /* null pointer, bad size, bad enum */
+    RT_ERR_NO_DEVICE = 2,     /* no HIP device / device index out of range */
+    RT_ERR_HIP = 3,           /* a HIP runtime call failed (rt_last_hip_error) */
+    RT_ERR_OUT_OF_MEMORY = 4,
+    RT_ERR_NO_SCENE = 5,      /* rt_render* before rt_set_scene */
+    RT_ERR_UNSUPPORTED = 6,   /* depth / flag combination this build does not ship */
+    RT_ERR_OUT_OF_RANGE = 7   /* row band outside the image (reference: std::out_of_range) */
+};
+
+/* ---- scene records (reference scene.h:35-84) ---------------------------- */
+
+/* Material — scene.h:35-49.  NOTE the reference constructor's positional order is
+ * (color, metallic, ambient, diffuse, specular, specular_exponent) with defaults
+ * .5/.1/.9/.4/50 (scene.h:48); the fields here are named, so order is irrelevant. */
+typedef struct rt_material {
+    double color[3];
+    double ambient;
+    double metallic;
+    double diffuse;
+    double specular;
+    double specular_exponent;
+} rt_material;
+
+enum rt_prim_kind {
+    RT_PRIM_SPHERE = 0,   /* Sphere, scene.h:75-84 */
+    RT_PRIM_WALL = 1      /* Wall,   scene.h:62-73 */
+};
+
+/* One SceneGeometry object, flattened.  Fields hold the OBJECT STATE, i.e. what the
+ * reference constructors store: Wall's normal is already normalised (scene.h:73
+ * normalises in the initialiser list), position is the wall's corner (scene.cpp:30). */
+typedef struct rt_prim {
+    int32_t kind;          /* rt_prim_kind */
+    int32_t reserved;      /* must be 0 */
+    rt_material mat;
+    double position[3];    /* Sphere::center | Wall::position */
+    double normal[3];      /* Wall::normal (unit); ignored for spheres */
+    double radius;         /* Sphere::radius */
+    double length;         /* Wall::length */
+    double width;          /* Wall::width */
+} rt_prim;
+
+/* The per-frame camera inputs of rt_scene (main.cpp:132-134): position plus the
+ * Camera::init outputs image_top_left and the returned {pixel_delta_x, pixel_delta_y}
+ * (scene.cpp:80-106).  They are passed explicitly (not recomputed from lookat)
+ * because the reference never re-calls init() after a camera move (main.cpp:154),
+ * so a moved camera keeps a stale image_top_left — a drop-in must reproduce that. */
+typedef struct rt_camera {
+    double position[3];
+    double image_top_left[3];
+    double pixel_delta_x[3];   /* u[0] in rt_scene */
+    double pixel_delta_y[3];   /* u[1] in rt_scene */
+    int32_t width;             /* cam.image_width */
+    int32_t height;            /* cam.image_height */
+} rt_camera;
+
+/* ---- render options ----------------------------------------------------- */
+enum rt_precision {
+    RT_PREC_F64 = 0,     /* fp64 everywhere, op-for-op the reference's arithmetic (parity) */
+    RT_PREC_F32 = 1,     /* fp32 everywhere (throughput; flips at discontinuities) */
+    RT_PREC_MIXED = 2    /* fp32 conservative cull + fp64 exact on survivors: output == F64 */
+};
+
+enum rt_out_format {
+    RT_OUT_RGB_F32 = 0,  /* H x W x 3 float, row-major, linear unclamped RGB (12 B/px) */
+    RT_OUT_RGB_F64 = 1,  /* H x W x 3 double (24 B/px) — exact drop-in for vector<vector<RGB>> */
+    RT_OUT_RGBA8 = 2     /* H x W x 4 uint8 (R,G,B,255): clamp(v,0,1)*255 truncated (main.cpp:345) */
+};
+
+enum rt_flags {
+    RT_FLAG_SUN = 1u << 0   /* build-defined sun term (SUN_COLOR/SUN_DIRECTION, main.cpp:18-19,
+                               defined but unused by the reference); off = reference parity */
+};
+
+typedef struct rt_stats {
+    double ms;             /* device time of the render (hipEvent), milliseconds */
+    uint64_t segments;     /* closest-hit queries issued (only when counting was asked) */
+} rt_stats;
+
+typedef struct rt_ctx rt_ctx;
+
+/* ---- lifecycle ---------------------------------------------------------- */
+int rt_ctx_create(int device, rt_ctx** out);
+int rt_ctx_destroy(rt_ctx* ctx);
+const char* rt_strerror(int status);
+const char* rt_last_hip_error(const rt_ctx* ctx);
+int rt_capi_version(void);
+
+/* ---- scene -------------------------------------------------------------- */
+/* Copies n primitives (in scene order: index j is the reference's scene.at(j)) to the
+ * device.  Replaces any previous scene.  n == 0 is a valid (empty) scene. */
+int rt_set_scene(rt_ctx* ctx, const rt_prim* prims, int32_t n);
+
+/* ---- frame operators (replace rt_scene, main.cpp:124-139) --------------- */
+/* Render rows [row0, row0+nrows) of the frame into caller-owned HOST memory `out`
+ * (nrows*width pixels of `out_format`), synchronously.  depth = remaining_iterations
+ * of recursive_ray_tracing (rt_scene passes the default 10, main.cpp:89/136).
+ * stats may be NULL; stats->segments is filled only when count_segments != 0. */
+int rt_render(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nrows, int32_t depth,
+              int32_t precision, uint32_t flags, int32_t out_format, void* out,
+              int32_t count_segments, rt_stats* stats);
+
+/* Same, but `d_out` is DEVICE memory and the launch is enqueued on `stream`
+ * (a hipStream_t; NULL = the ctx's stream) without synchronising: the hot path as a
+ * bench or a multi-GPU tiler drives it.  If d_segments != NULL it must point to one
+ * device uint64 that receives += the segment count. */
+int rt_render_device(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nrows,
+                     int32_t depth, int32_t precision, uint32_t flags, int32_t out_format,
+                     void* d_out, uint64_t* d_segments, void* stream);
+
+/* ---- host helpers (restatements the host side of rt_scene needs) -------- */
+/* Camera::init (scene.cpp:80-106) in fp64: fills cam from the Camera fields.
+ * height = (int)(image_width / aspect_ratio) exactly as scene.cpp:82. */
+int rt_camera_init(const double position[3], const double lookat[3], const double vup[3],
+                   double vfov, double aspect_ratio, double image_width, rt_camera* cam);
+
+/* Bytes per pixel of an output format (0 for an unknown format). */
+int32_t rt_out_bytes_per_pixel(int32_t out_format);
+
+/* Row band owned by `rank` of `nranks` when the frame is split into contiguous
+ * blocks for multi-GPU tiling: [*row0, *row0 + *nrows). */
+int rt_band_rows(int32_t height, int32_t nranks, int32_t rank, int32_t* row0, int32_t* nrows);
+
+/* Largest depth the kernels are compiled for (depth 0..RT_MAX_DEPTH). */
+int32_t rt_max_depth(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT_CAPI_H */

@@ -1,0 +1,195 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes binding of the oracle (liboracle.so) and, where it
+was built, of the reference harness (_ref/libref.so).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this module,
+and only as the checker / the timed CPU baseline; the product path never does.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+ORACLE_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(ORACLE_DIR)
+sys.path.insert(0, os.path.join(REPO, "ray-tracer-from-scratch_amd"))
+from rtamd import capi  # noqa: E402  (struct definitions only; no compute)
+
+ORACLE_LIB = os.path.join(ORACLE_DIR, "liboracle.so")
+REF_LIB = os.path.join(ORACLE_DIR, "_ref", "libref.so")
+
+_P = C.POINTER
+_dp = _P(C.c_double)
+_prim_p = _P(capi.rt_prim)
+
+
+def build(ref: bool = False) -> None:
+    targets = ["all"] + (["ref"] if ref else [])
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR] + targets, check=True)
+
+
+def _arr(v, n=3):
+    return (C.c_double * n)(*[float(x) for x in v])
+
+
+class Oracle:
+    """fp64 C restatement of the reference hot path (rt_oracle.c)."""
+
+    def __init__(self, path: str = ORACLE_LIB):
+        if not os.path.exists(path):
+            build()
+        lib = C.CDLL(path)
+        sig = {
+            "orc_sphere_intersect": (None, [_prim_p, _dp, _dp, _dp, _dp, _P(C.c_int)]),
+            "orc_wall_intersect": (None, [_prim_p, _dp, _dp, _dp, _dp, _P(C.c_int)]),
+            "orc_out_color": (None, [_dp, _dp]),
+            "orc_diffuse_shading": (C.c_double, [_dp, _dp, _dp]),
+            "orc_specular": (C.c_double, [_dp, _dp, _dp, _dp]),
+            "orc_reflect": (None, [_dp, _dp, _dp]),
+            "orc_find_closest_hit": (C.c_int, [_prim_p, C.c_int, _dp, _dp, _dp, _dp]),
+            "orc_trace": (None, [_prim_p, C.c_int, _dp, _dp, C.c_int, C.c_uint32, _dp,
+                                 _P(C.c_uint64)]),
+            "orc_camera_init": (C.c_int, [_dp, _dp, _dp, C.c_double, C.c_double, C.c_double,
+                                          _P(capi.rt_camera)]),
+            "orc_render": (C.c_uint64, [_prim_p, C.c_int, _P(capi.rt_camera), C.c_int, C.c_int,
+                                        C.c_int, C.c_uint32, _dp, _P(C.c_float),
+                                        _P(C.c_uint64), C.c_int]),
+            "orc_synthetic_scene": (C.c_int, [C.c_int, C.c_int, C.c_uint64, _prim_p, _dp]),
+            "orc_default_scene": (C.c_int, [_prim_p, _dp]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(lib, name)
+            f.restype = res
+            f.argtypes = args
+        self.lib = lib
+
+    @staticmethod
+    def prim_array(prims):
+        return (capi.rt_prim * max(1, len(prims)))(*prims)
+
+    def camera_init(self, position, lookat, vup, vfov, aspect_ratio, image_width):
+        cam = capi.rt_camera()
+        self.lib.orc_camera_init(_arr(position), _arr(lookat), _arr(vup), vfov, aspect_ratio,
+                                 image_width, C.byref(cam))
+        return cam
+
+    def render(self, prims, cam, depth, flags=0, row0=0, nrows=None, nthreads=0, want64=True,
+               want_sig=False):
+        """-> (rgb64 [nrows,W,3] or None, rgb32 [nrows,W,3], segments[, path_sig [nrows,W]])"""
+        if nrows is None:
+            nrows = cam.height - row0
+        arr = self.prim_array(prims)
+        out32 = np.empty((nrows, cam.width, 3), np.float32)
+        out64 = np.empty((nrows, cam.width, 3), np.float64) if want64 else None
+        sig = np.empty((nrows, cam.width), np.uint64) if want_sig else None
+        segs = self.lib.orc_render(
+            arr, len(prims), C.byref(cam), row0, nrows, depth, flags,
+            out64.ctypes.data_as(_dp) if want64 else None,
+            out32.ctypes.data_as(_P(C.c_float)),
+            sig.ctypes.data_as(_P(C.c_uint64)) if want_sig else None, nthreads)
+        if want_sig:
+            return out64, out32, int(segs), sig
+        return out64, out32, int(segs)
+
+    def trace(self, prims, o, d, depth, flags=0):
+        rgb = (C.c_double * 3)()
+        segs = C.c_uint64()
+        self.lib.orc_trace(self.prim_array(prims), len(prims), _arr(o), _arr(d), depth, flags,
+                           rgb, C.byref(segs))
+        return tuple(rgb), segs.value
+
+    def sphere_intersect(self, prim, o, d):
+        dist, n, hit = C.c_double(), (C.c_double * 3)(), C.c_int()
+        self.lib.orc_sphere_intersect(C.byref(prim), _arr(o), _arr(d), C.byref(dist), n,
+                                      C.byref(hit))
+        return dist.value, tuple(n), hit.value
+
+    def wall_intersect(self, prim, o, d):
+        dist, n, hit = C.c_double(), (C.c_double * 3)(), C.c_int()
+        self.lib.orc_wall_intersect(C.byref(prim), _arr(o), _arr(d), C.byref(dist), n,
+                                    C.byref(hit))
+        return dist.value, tuple(n), hit.value
+
+    def out_color(self, v):
+        rgb = (C.c_double * 3)()
+        self.lib.orc_out_color(_arr(v), rgb)
+        return tuple(rgb)
+
+    def diffuse_shading(self, pos, normal, light):
+        return self.lib.orc_diffuse_shading(_arr(pos), _arr(normal), _arr(light))
+
+    def specular(self, pos, normal, light, view):
+        return self.lib.orc_specular(_arr(pos), _arr(normal), _arr(light), _arr(view))
+
+    def reflect(self, v, n):
+        out = (C.c_double * 3)()
+        self.lib.orc_reflect(_arr(v), _arr(n), out)
+        return tuple(out)
+
+    def find_closest_hit(self, prims, o, d):
+        dist, n = C.c_double(), (C.c_double * 3)()
+        idx = self.lib.orc_find_closest_hit(self.prim_array(prims), len(prims), _arr(o), _arr(d),
+                                            C.byref(dist), n)
+        return idx, dist.value, tuple(n)
+
+    def synthetic_scene(self, n_spheres, n_walls, seed=1234):
+        arr = (capi.rt_prim * max(1, n_spheres + n_walls))()
+        raw = (C.c_double * max(3, 3 * n_walls))()
+        n = self.lib.orc_synthetic_scene(n_spheres, n_walls, seed, arr, raw)
+        return [arr[i] for i in range(n)], list(raw)[:3 * n_walls]
+
+
+class Reference:
+    """The reference's own compiled code (oracle/_ref/libref.so; this container only)."""
+
+    def __init__(self, path: str = REF_LIB):
+        if not os.path.exists(path):
+            raise FileNotFoundError(path)
+        lib = C.CDLL(path)
+        sig = {
+            "ref_camera_init": (C.c_int, [_dp, _dp, _dp, C.c_double, C.c_double, C.c_double, _dp]),
+            "ref_render": (C.c_int, [_prim_p, _dp, C.c_int, _dp, _dp, _dp, C.c_double, C.c_double,
+                                     C.c_double, C.c_int, _dp]),
+            "ref_rt_scene_wh_alloc": (C.c_int, [_prim_p, _dp, C.c_int, _dp, _dp, _dp, C.c_double,
+                                                C.c_double, C.c_double]),
+            "ref_trace": (C.c_int, [_prim_p, _dp, C.c_int, _dp, _dp, C.c_int, _dp]),
+            "ref_find_closest_hit": (C.c_int, [_prim_p, _dp, C.c_int, _dp, _dp, _dp, _dp]),
+            "ref_sphere_intersect": (None, [_dp, C.c_double, _dp, _dp, _dp, _dp, _P(C.c_int)]),
+            "ref_wall_intersect": (None, [_dp, _dp, C.c_double, C.c_double, _dp, _dp, _dp, _dp,
+                                          _P(C.c_int)]),
+            "ref_out_color": (None, [_dp, _dp]),
+            "ref_diffuse_shading": (C.c_double, [_dp, _dp, _dp]),
+            "ref_specular": (C.c_double, [_dp, _dp, _dp, _dp]),
+            "ref_reflect": (None, [_dp, _dp, _dp]),
+            "ref_normalize": (None, [_dp, _dp]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(lib, name)
+            f.restype = res
+            f.argtypes = args
+        self.lib = lib
+
+    @staticmethod
+    def available() -> bool:
+        return os.path.exists(REF_LIB)
+
+    def camera_init(self, position, lookat, vup, vfov, aspect_ratio, image_width):
+        out = (C.c_double * 12)()
+        h = self.lib.ref_camera_init(_arr(position), _arr(lookat), _arr(vup), vfov, aspect_ratio,
+                                     image_width, out)
+        return h, np.array(list(out)).reshape(4, 3)
+
+    def render(self, prims, raw, cam_args, depth):
+        W = int(cam_args["image_width"])
+        H = int(W / cam_args["aspect_ratio"])
+        out = np.empty((H, W, 3), np.float64)
+        rawa = _arr(raw if raw else [0.0] * 3, max(3, len(raw)))
+        h = self.lib.ref_render(Oracle.prim_array(prims), rawa, len(prims),
+                                _arr(cam_args["position"]), _arr(cam_args["lookat"]),
+                                _arr(cam_args["vup"]), cam_args["vfov"], cam_args["aspect_ratio"],
+                                cam_args["image_width"], depth, out.ctypes.data_as(_dp))
+        assert h == H, (h, H)
+        return out

@@ -1,0 +1,367 @@
+/*
+ * rt_capi.cpp — implementation of include/rt_capi.h (host side, HIP runtime).
+ *
+ * Owns the device scene (one HBM allocation in the layout of rt_device.h), a stream,
+ * timing events and a staging buffer for host-output renders.  No exception crosses
+ * the boundary; every entry point returns an rt_status.
+ */
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "../../include/rt_capi.h"
+#include "rt_device.h"
+
+struct rt_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    void* d_scene = nullptr;
+    size_t scene_bytes = 0;
+    bool have_scene = false;
+    int nS = 0, nW = 0, nP = 0;
+    size_t off_wall = 0, off_mat = 0;
+    void* d_out = nullptr;
+    size_t d_out_cap = 0;
+    unsigned long long* d_segs = nullptr;
+    char last_err[256] = {0};
+};
+
+namespace {
+
+int hip_fail(rt_ctx* ctx, hipError_t e, const char* what) {
+    if (ctx)
+        std::snprintf(ctx->last_err, sizeof ctx->last_err, "%s: %s", what, hipGetErrorString(e));
+    return e == hipErrorOutOfMemory ? RT_ERR_OUT_OF_MEMORY : RT_ERR_HIP;
+}
+
+#define RT_HIP(ctx, call)                                   \
+    do {                                                    \
+        hipError_t e_ = (call);                             \
+        if (e_ != hipSuccess) return hip_fail(ctx, e_, #call); \
+    } while (0)
+
+/* vec.cpp restatements used to pack Wall invariants (same fp64 operations). */
+struct hv3 {
+    double x, y, z;
+};
+hv3 hcross(hv3 u, hv3 v) {  // vec.cpp:15
+    return {u.y * v.z - u.z * v.y, u.z * v.x - u.x * v.z, u.x * v.y - u.y * v.x};
+}
+hv3 hnormalize(hv3 v) {  // vec.cpp:21 (v / length())
+    double l = std::sqrt(v.x * v.x + v.y * v.y + v.z * v.z);
+    return {v.x / l, v.y / l, v.z / l};
+}
+bool hnan(hv3 v) { return std::isnan(v.x) || std::isnan(v.y) || std::isnan(v.z); }
+
+size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+int bytes_per_pixel(int32_t f) {
+    switch (f) {
+        case RT_OUT_RGB_F32: return 12;
+        case RT_OUT_RGB_F64: return 24;
+        case RT_OUT_RGBA8: return 4;
+        default: return 0;
+    }
+}
+
+int check_render_args(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nrows,
+                      int32_t depth, int32_t precision, int32_t out_format) {
+    if (!ctx || !cam) return RT_ERR_INVALID_ARG;
+    if (!ctx->have_scene) return RT_ERR_NO_SCENE;
+    if (cam->width < 0 || cam->height < 0 || nrows < 0) return RT_ERR_INVALID_ARG;
+    if (row0 < 0 || row0 + nrows > cam->height) return RT_ERR_OUT_OF_RANGE;
+    if (depth < 0) return RT_ERR_INVALID_ARG;
+    if (depth > rt::max_depth()) return RT_ERR_UNSUPPORTED;
+    if (precision < RT_PREC_F64 || precision > RT_PREC_MIXED) return RT_ERR_INVALID_ARG;
+    if (bytes_per_pixel(out_format) == 0) return RT_ERR_INVALID_ARG;
+    return RT_OK;
+}
+
+rt::KParams make_params(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nrows,
+                        int32_t depth, uint32_t flags, int32_t out_format, void* d_out,
+                        unsigned long long* d_segs) {
+    rt::KParams p{};
+    const char* base = static_cast<const char*>(ctx->d_scene);
+    p.sph = reinterpret_cast<const rt::DevSphere*>(base);
+    p.wal = reinterpret_cast<const rt::DevWall*>(base + ctx->off_wall);
+    p.mat = reinterpret_cast<const rt::DevMat*>(base + ctx->off_mat);
+    p.nS = ctx->nS;
+    p.nW = ctx->nW;
+    p.nP = ctx->nP;
+    p.W = cam->width;
+    p.row0 = row0;
+    p.nrows = nrows;
+    p.depth = depth;
+    p.flags = flags;
+    p.outf = out_format;
+    for (int k = 0; k < 3; k++) {
+        p.pos[k] = cam->position[k];
+        p.tl[k] = cam->image_top_left[k];
+        p.dx[k] = cam->pixel_delta_x[k];
+        p.dy[k] = cam->pixel_delta_y[k];
+    }
+    p.out = d_out;
+    p.segs = d_segs;
+    return p;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_capi_version(void) { return RT_CAPI_VERSION; }
+
+const char* rt_strerror(int status) {
+    switch (status) {
+        case RT_OK: return "ok";
+        case RT_ERR_INVALID_ARG: return "invalid argument";
+        case RT_ERR_NO_DEVICE: return "no HIP device";
+        case RT_ERR_HIP: return "HIP runtime error";
+        case RT_ERR_OUT_OF_MEMORY: return "out of device memory";
+        case RT_ERR_NO_SCENE: return "no scene uploaded";
+        case RT_ERR_UNSUPPORTED: return "unsupported depth/flags";
+        case RT_ERR_OUT_OF_RANGE: return "row band out of range";
+        default: return "unknown status";
+    }
+}
+
+const char* rt_last_hip_error(const rt_ctx* ctx) { return ctx ? ctx->last_err : ""; }
+
+int32_t rt_out_bytes_per_pixel(int32_t out_format) { return bytes_per_pixel(out_format); }
+
+int32_t rt_max_depth(void) { return rt::max_depth(); }
+
+int rt_band_rows(int32_t height, int32_t nranks, int32_t rank, int32_t* row0, int32_t* nrows) {
+    if (!row0 || !nrows || height < 0 || nranks <= 0 || rank < 0 || rank >= nranks)
+        return RT_ERR_INVALID_ARG;
+    // contiguous blocks, the first (height % nranks) ranks take one extra row
+    const int32_t base = height / nranks, extra = height % nranks;
+    *row0 = rank * base + (rank < extra ? rank : extra);
+    *nrows = base + (rank < extra ? 1 : 0);
+    return RT_OK;
+}
+
+int rt_camera_init(const double position[3], const double lookat[3], const double vup[3],
+                   double vfov, double aspect_ratio, double image_width, rt_camera* cam) {
+    /* Camera::init, scene.cpp:80-106, op for op (3.14 for pi kept). */
+    if (!position || !lookat || !vup || !cam) return RT_ERR_INVALID_ARG;
+    const hv3 pos{position[0], position[1], position[2]};
+    const hv3 look{lookat[0], lookat[1], lookat[2]};
+    const hv3 up{vup[0], vup[1], vup[2]};
+    const double image_height = static_cast<int>(image_width / aspect_ratio);
+    const hv3 pl{pos.x - look.x, pos.y - look.y, pos.z - look.z};
+    const double focal_length = std::sqrt(pl.x * pl.x + pl.y * pl.y + pl.z * pl.z);
+    const double theta = vfov * 3.14 / 180.0;
+    const double h = std::tan(theta / 2);
+    const double fov_height = 2 * h * focal_length;
+    const double fov_width = fov_height * (static_cast<double>(image_width) / image_height);
+    const hv3 w = hnormalize(pl);
+    const hv3 u = hnormalize(hcross(up, w));
+    const hv3 v = hcross(w, u);
+    const hv3 fx{u.x * fov_width, u.y * fov_width, u.z * fov_width};
+    const double nfh = -fov_height;
+    const hv3 fy{v.x * nfh, v.y * nfh, v.z * nfh};
+    const hv3 pdx{fx.x / image_width, fx.y / image_width, fx.z / image_width};
+    const hv3 pdy{fy.x / image_height, fy.y / image_height, fy.z / image_height};
+    const hv3 wf{w.x * focal_length, w.y * focal_length, w.z * focal_length};
+    const hv3 ftl{((pos.x - wf.x) - fx.x / 2) - fy.x / 2, ((pos.y - wf.y) - fx.y / 2) - fy.y / 2,
+                  ((pos.z - wf.z) - fx.z / 2) - fy.z / 2};
+    const hv3 s{pdx.x + pdy.x, pdx.y + pdy.y, pdx.z + pdy.z};
+    const hv3 itl{ftl.x + s.x * 0.5, ftl.y + s.y * 0.5, ftl.z + s.z * 0.5};
+    const double p3[4][3] = {{pos.x, pos.y, pos.z}, {itl.x, itl.y, itl.z},
+                             {pdx.x, pdx.y, pdx.z}, {pdy.x, pdy.y, pdy.z}};
+    std::memcpy(cam->position, p3[0], sizeof p3[0]);
+    std::memcpy(cam->image_top_left, p3[1], sizeof p3[1]);
+    std::memcpy(cam->pixel_delta_x, p3[2], sizeof p3[2]);
+    std::memcpy(cam->pixel_delta_y, p3[3], sizeof p3[3]);
+    cam->width = static_cast<int32_t>(image_width);
+    cam->height = static_cast<int32_t>(image_height);
+    return RT_OK;
+}
+
+int rt_ctx_create(int device, rt_ctx** out) {
+    if (!out) return RT_ERR_INVALID_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return RT_ERR_NO_DEVICE;
+    if (device < 0 || device >= n) return RT_ERR_NO_DEVICE;
+    rt_ctx* ctx = new (std::nothrow) rt_ctx();
+    if (!ctx) return RT_ERR_OUT_OF_MEMORY;
+    ctx->device = device;
+    int st = RT_OK;
+    do {
+        hipError_t e;
+        if ((e = hipSetDevice(device)) != hipSuccess) { st = hip_fail(ctx, e, "hipSetDevice"); break; }
+        if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess) {
+            st = hip_fail(ctx, e, "hipStreamCreate"); break;
+        }
+        if ((e = hipEventCreate(&ctx->ev0)) != hipSuccess) { st = hip_fail(ctx, e, "hipEventCreate"); break; }
+        if ((e = hipEventCreate(&ctx->ev1)) != hipSuccess) { st = hip_fail(ctx, e, "hipEventCreate"); break; }
+        if ((e = hipMalloc(&ctx->d_segs, sizeof(unsigned long long))) != hipSuccess) {
+            st = hip_fail(ctx, e, "hipMalloc(segs)"); break;
+        }
+    } while (0);
+    if (st != RT_OK) {
+        rt_ctx_destroy(ctx);
+        return st;
+    }
+    *out = ctx;
+    return RT_OK;
+}
+
+int rt_ctx_destroy(rt_ctx* ctx) {
+    if (!ctx) return RT_ERR_INVALID_ARG;
+    hipSetDevice(ctx->device);
+    if (ctx->stream) hipStreamSynchronize(ctx->stream);
+    if (ctx->d_scene) hipFree(ctx->d_scene);
+    if (ctx->d_out) hipFree(ctx->d_out);
+    if (ctx->d_segs) hipFree(ctx->d_segs);
+    if (ctx->ev0) hipEventDestroy(ctx->ev0);
+    if (ctx->ev1) hipEventDestroy(ctx->ev1);
+    if (ctx->stream) hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return RT_OK;
+}
+
+int rt_set_scene(rt_ctx* ctx, const rt_prim* prims, int32_t n) {
+    if (!ctx || n < 0 || (n > 0 && !prims)) return RT_ERR_INVALID_ARG;
+    std::vector<rt::DevSphere> sph;
+    std::vector<rt::DevWall> wal;
+    std::vector<rt::DevMat> mat((size_t)n);
+    for (int32_t j = 0; j < n; j++) {
+        const rt_prim& q = prims[j];
+        if (q.reserved != 0) return RT_ERR_INVALID_ARG;
+        rt::DevMat& m = mat[(size_t)j];
+        for (int k = 0; k < 3; k++) m.color[k] = q.mat.color[k];
+        m.ka = q.mat.ambient;
+        m.km = q.mat.metallic;
+        m.kd = q.mat.diffuse;
+        m.ks = q.mat.specular;
+        m.ex = q.mat.specular_exponent;
+        if (q.kind == RT_PRIM_SPHERE) {
+            rt::DevSphere s{};
+            for (int k = 0; k < 3; k++) {
+                s.c[k] = q.position[k];
+                s.cf[k] = (float)q.position[k];
+            }
+            s.r2 = q.radius * q.radius;  // scene.cpp:51
+            s.r2f = (float)s.r2;
+            s.rf = (float)q.radius;
+            s.j = j;
+            sph.push_back(s);
+        } else if (q.kind == RT_PRIM_WALL) {
+            const hv3 nrm{q.normal[0], q.normal[1], q.normal[2]};
+            const hv3 X = hnormalize(hcross(nrm, hv3{0, 0, 1}));  // scene.cpp:18
+            const hv3 Y = hnormalize(hcross(X, nrm));             // scene.cpp:19
+            // A NaN basis (normal parallel to z) or NaN normal makes every projection NaN:
+            // the reference can never report a hit for this wall, so it is not uploaded.
+            if (hnan(X) || hnan(Y) || hnan(nrm)) continue;
+            rt::DevWall w{};
+            const double Xa[3] = {X.x, X.y, X.z}, Ya[3] = {Y.x, Y.y, Y.z};
+            for (int k = 0; k < 3; k++) {
+                w.P[k] = q.position[k];
+                w.n[k] = q.normal[k];
+                w.X[k] = Xa[k];
+                w.Y[k] = Ya[k];
+                w.Pf[k] = (float)q.position[k];
+                w.nf[k] = (float)q.normal[k];
+                w.Xf[k] = (float)Xa[k];
+                w.Yf[k] = (float)Ya[k];
+            }
+            w.len = q.length;
+            w.wid = q.width;
+            w.lenf = (float)q.length;
+            w.widf = (float)q.width;
+            w.j = j;
+            wal.push_back(w);
+        } else {
+            return RT_ERR_INVALID_ARG;
+        }
+    }
+    const size_t bs = sph.size() * sizeof(rt::DevSphere);
+    const size_t off_wall = align_up(bs, 256);
+    const size_t off_mat = align_up(off_wall + wal.size() * sizeof(rt::DevWall), 256);
+    const size_t total = align_up(off_mat + mat.size() * sizeof(rt::DevMat), 256) + 256;
+    std::vector<char> host(total, 0);
+    if (!sph.empty()) std::memcpy(host.data(), sph.data(), bs);
+    if (!wal.empty()) std::memcpy(host.data() + off_wall, wal.data(), wal.size() * sizeof(rt::DevWall));
+    if (!mat.empty()) std::memcpy(host.data() + off_mat, mat.data(), mat.size() * sizeof(rt::DevMat));
+
+    RT_HIP(ctx, hipSetDevice(ctx->device));
+    RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (total > ctx->scene_bytes) {
+        if (ctx->d_scene) RT_HIP(ctx, hipFree(ctx->d_scene));
+        ctx->d_scene = nullptr;
+        ctx->scene_bytes = 0;
+        RT_HIP(ctx, hipMalloc(&ctx->d_scene, total));
+        ctx->scene_bytes = total;
+    }
+    RT_HIP(ctx, hipMemcpy(ctx->d_scene, host.data(), total, hipMemcpyHostToDevice));
+    ctx->nS = (int)sph.size();
+    ctx->nW = (int)wal.size();
+    ctx->nP = n;
+    ctx->off_wall = off_wall;
+    ctx->off_mat = off_mat;
+    ctx->have_scene = true;
+    return RT_OK;
+}
+
+int rt_render_device(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nrows,
+                     int32_t depth, int32_t precision, uint32_t flags, int32_t out_format,
+                     void* d_out, uint64_t* d_segments, void* stream) {
+    int st = check_render_args(ctx, cam, row0, nrows, depth, precision, out_format);
+    if (st != RT_OK) return st;
+    if (!d_out && nrows > 0 && cam->width > 0) return RT_ERR_INVALID_ARG;
+    const rt::KParams p = make_params(ctx, cam, row0, nrows, depth, flags, out_format, d_out,
+                                      reinterpret_cast<unsigned long long*>(d_segments));
+    void* s = stream ? stream : static_cast<void*>(ctx->stream);
+    const int e = rt::launch_trace(p, precision, s);
+    if (e != (int)hipSuccess) return hip_fail(ctx, (hipError_t)e, "launch k_trace");
+    return RT_OK;
+}
+
+int rt_render(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nrows, int32_t depth,
+              int32_t precision, uint32_t flags, int32_t out_format, void* out,
+              int32_t count_segments, rt_stats* stats) {
+    int st = check_render_args(ctx, cam, row0, nrows, depth, precision, out_format);
+    if (st != RT_OK) return st;
+    const size_t bytes = (size_t)nrows * (size_t)cam->width * (size_t)bytes_per_pixel(out_format);
+    if (!out && bytes > 0) return RT_ERR_INVALID_ARG;
+    RT_HIP(ctx, hipSetDevice(ctx->device));
+    if (bytes > ctx->d_out_cap) {
+        RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        if (ctx->d_out) RT_HIP(ctx, hipFree(ctx->d_out));
+        ctx->d_out = nullptr;
+        ctx->d_out_cap = 0;
+        RT_HIP(ctx, hipMalloc(&ctx->d_out, bytes));
+        ctx->d_out_cap = bytes;
+    }
+    unsigned long long* segs = count_segments ? ctx->d_segs : nullptr;
+    if (segs) RT_HIP(ctx, hipMemsetAsync(segs, 0, sizeof *segs, ctx->stream));
+    RT_HIP(ctx, hipEventRecord(ctx->ev0, ctx->stream));
+    const rt::KParams p = make_params(ctx, cam, row0, nrows, depth, flags, out_format,
+                                      ctx->d_out, segs);
+    const int e = rt::launch_trace(p, precision, ctx->stream);
+    if (e != (int)hipSuccess) return hip_fail(ctx, (hipError_t)e, "launch k_trace");
+    RT_HIP(ctx, hipEventRecord(ctx->ev1, ctx->stream));
+    if (bytes > 0)
+        RT_HIP(ctx, hipMemcpyAsync(out, ctx->d_out, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    unsigned long long hsegs = 0;
+    if (segs)
+        RT_HIP(ctx, hipMemcpyAsync(&hsegs, segs, sizeof hsegs, hipMemcpyDeviceToHost, ctx->stream));
+    RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (stats) {
+        float ms = 0.f;
+        RT_HIP(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+        stats->ms = ms;
+        stats->segments = hsegs;
+    }
+    return RT_OK;
+}
+
+}  // extern "C"

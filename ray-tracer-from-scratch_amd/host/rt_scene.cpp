@@ -1,0 +1,94 @@
+/*
+ * host/rt_scene.cpp — the drop-in frame operator (main.cpp:124-139) on the GPU path.
+ *
+ * Same signature and observable behaviour as the reference: fills
+ * frame_buffer.at(i).at(j) for every row i < image_height and column j < image_width,
+ * with RGB values of recursive_ray_tracing at depth 10.  Underneath, the scene is
+ * flattened through SceneGeometry::pack() and rendered by the HIP kernel through the
+ * C-ABI with fp64 output (RT_OUT_RGB_F64), so the values are the fp64 path's.
+ *
+ * The reference has no context argument, so a process-wide renderer is created on first
+ * use (device/precision from rt_scene_set_options); like the reference, rt_scene is
+ * meant to be called from one thread.
+ */
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/rt/scene.h"
+
+namespace {
+
+struct Global {
+    std::mutex mu;
+    RtSceneOptions opts;
+    rt_ctx* ctx = nullptr;
+    int ctx_device = -1;
+    std::vector<double> staging;
+    ~Global() {
+        if (ctx) rt_ctx_destroy(ctx);
+    }
+};
+
+Global& global() {
+    static Global g;
+    return g;
+}
+
+void check(int st, rt_ctx* ctx, const char* what) {
+    if (st != RT_OK)
+        throw std::runtime_error(std::string(what) + ": " + rt_strerror(st) + " " +
+                                 rt_last_hip_error(ctx));
+}
+
+}  // namespace
+
+void rt_scene_set_options(const RtSceneOptions& opts) {
+    Global& g = global();
+    std::lock_guard<std::mutex> lk(g.mu);
+    g.opts = opts;
+}
+
+RtSceneOptions rt_scene_get_options() {
+    Global& g = global();
+    std::lock_guard<std::mutex> lk(g.mu);
+    return g.opts;
+}
+
+void rt_scene(std::vector<vec3> u, const std::vector<std::unique_ptr<SceneGeometry>>& scene,
+              const Camera& cam, std::vector<std::vector<RGB>>& frame_buffer) {
+    Global& g = global();
+    std::lock_guard<std::mutex> lk(g.mu);
+    if (!g.ctx || g.ctx_device != g.opts.device) {
+        if (g.ctx) rt_ctx_destroy(g.ctx);
+        g.ctx = nullptr;
+        check(rt_ctx_create(g.opts.device, &g.ctx), nullptr, "rt_ctx_create");
+        g.ctx_device = g.opts.device;
+    }
+    std::vector<rt_prim> prims(scene.size());
+    for (size_t j = 0; j < scene.size(); j++) scene[j]->pack(&prims[j]);
+    check(rt_set_scene(g.ctx, prims.data(), (int32_t)prims.size()), g.ctx, "rt_set_scene");
+
+    rt_camera c{};
+    const vec3* v[4] = {&cam.position, &cam.image_top_left, &u.at(0), &u.at(1)};
+    double* dst[4] = {c.position, c.image_top_left, c.pixel_delta_x, c.pixel_delta_y};
+    for (int k = 0; k < 4; k++) {
+        dst[k][0] = v[k]->x;
+        dst[k][1] = v[k]->y;
+        dst[k][2] = v[k]->z;
+    }
+    const int W = (int)cam.image_width, H = (int)cam.image_height;
+    c.width = W;
+    c.height = H;
+    g.staging.resize((size_t)W * H * 3);
+    check(rt_render(g.ctx, &c, 0, H, g.opts.depth, g.opts.precision, g.opts.flags,
+                    RT_OUT_RGB_F64, g.staging.data(), 0, nullptr),
+          g.ctx, "rt_render");
+    for (int i = 0; i < H; i++)
+        for (int j = 0; j < W; j++) {
+            const double* p = &g.staging[((size_t)i * W + j) * 3];
+            frame_buffer.at(i).at(j) = RGB(p[0], p[1], p[2]);  // main.cpp:136 indexing
+        }
+}

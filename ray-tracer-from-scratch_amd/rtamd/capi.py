@@ -1,0 +1,235 @@
+"""ctypes binding of include/rt_capi.h (the C-ABI drop-in boundary).
+
+This is the binding a Python host would add; bench.py and the GPU parity tests drive the
+HIP path through it.  The library is loaded from the in-tree build
+(ray-tracer-from-scratch_amd/lib/librt_amd.so); a missing library raises — there is no
+CPU fallback on the product path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_DIR = os.path.join(PKG_DIR, "lib")
+LIB_PATH = os.path.join(LIB_DIR, "librt_amd.so")
+HOST_LIB_PATH = os.path.join(LIB_DIR, "librt_host.so")
+
+# ---- enums (rt_capi.h) ----------------------------------------------------
+RT_OK = 0
+RT_ERR_INVALID_ARG = 1
+RT_ERR_NO_DEVICE = 2
+RT_ERR_HIP = 3
+RT_ERR_OUT_OF_MEMORY = 4
+RT_ERR_NO_SCENE = 5
+RT_ERR_UNSUPPORTED = 6
+RT_ERR_OUT_OF_RANGE = 7
+
+RT_PRIM_SPHERE = 0
+RT_PRIM_WALL = 1
+
+RT_PREC_F64 = 0
+RT_PREC_F32 = 1
+RT_PREC_MIXED = 2
+PRECISIONS = {"f64": RT_PREC_F64, "f32": RT_PREC_F32, "mixed": RT_PREC_MIXED}
+
+RT_OUT_RGB_F32 = 0
+RT_OUT_RGB_F64 = 1
+RT_OUT_RGBA8 = 2
+
+RT_FLAG_SUN = 1
+
+
+class rt_material(C.Structure):
+    _fields_ = [
+        ("color", C.c_double * 3),
+        ("ambient", C.c_double),
+        ("metallic", C.c_double),
+        ("diffuse", C.c_double),
+        ("specular", C.c_double),
+        ("specular_exponent", C.c_double),
+    ]
+
+
+class rt_prim(C.Structure):
+    _fields_ = [
+        ("kind", C.c_int32),
+        ("reserved", C.c_int32),
+        ("mat", rt_material),
+        ("position", C.c_double * 3),
+        ("normal", C.c_double * 3),
+        ("radius", C.c_double),
+        ("length", C.c_double),
+        ("width", C.c_double),
+    ]
+
+
+class rt_camera(C.Structure):
+    _fields_ = [
+        ("position", C.c_double * 3),
+        ("image_top_left", C.c_double * 3),
+        ("pixel_delta_x", C.c_double * 3),
+        ("pixel_delta_y", C.c_double * 3),
+        ("width", C.c_int32),
+        ("height", C.c_int32),
+    ]
+
+
+class rt_stats(C.Structure):
+    _fields_ = [("ms", C.c_double), ("segments", C.c_uint64)]
+
+
+# Every entry point include/rt_capi.h declares: (name, restype, argtypes).
+_dbl3 = C.POINTER(C.c_double)
+SIGNATURES = [
+    ("rt_ctx_create", C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
+    ("rt_ctx_destroy", C.c_int, [C.c_void_p]),
+    ("rt_strerror", C.c_char_p, [C.c_int]),
+    ("rt_last_hip_error", C.c_char_p, [C.c_void_p]),
+    ("rt_capi_version", C.c_int, []),
+    ("rt_set_scene", C.c_int, [C.c_void_p, C.POINTER(rt_prim), C.c_int32]),
+    ("rt_render", C.c_int,
+     [C.c_void_p, C.POINTER(rt_camera), C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+      C.c_uint32, C.c_int32, C.c_void_p, C.c_int32, C.POINTER(rt_stats)]),
+    ("rt_render_device", C.c_int,
+     [C.c_void_p, C.POINTER(rt_camera), C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+      C.c_uint32, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]),
+    ("rt_camera_init", C.c_int,
+     [_dbl3, _dbl3, _dbl3, C.c_double, C.c_double, C.c_double, C.POINTER(rt_camera)]),
+    ("rt_out_bytes_per_pixel", C.c_int32, [C.c_int32]),
+    ("rt_band_rows", C.c_int,
+     [C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    ("rt_max_depth", C.c_int32, []),
+]
+
+_lib = None
+
+
+class RTError(RuntimeError):
+    def __init__(self, status: int, detail: str = ""):
+        self.status = status
+        msg = f"rt status {status}"
+        if _lib is not None:
+            msg += f" ({_lib.rt_strerror(status).decode()})"
+        if detail:
+            msg += f": {detail}"
+        super().__init__(msg)
+
+
+def load(path: str | None = None) -> C.CDLL:
+    """Load librt_amd.so (raises if it was not built — the product has no fallback)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise FileNotFoundError(
+            f"{p} not built: run `make -C ray-tracer-from-scratch_amd` (or __graft_entry__.build())")
+    lib = C.CDLL(p)
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def check(status: int, ctx=None) -> None:
+    if status != RT_OK:
+        detail = ""
+        if ctx is not None and _lib is not None:
+            detail = (_lib.rt_last_hip_error(ctx) or b"").decode()
+        raise RTError(status, detail)
+
+
+def _d3(v) -> C.Array:
+    return (C.c_double * 3)(*[float(x) for x in v])
+
+
+def camera_init(position, lookat, vup, vfov: float, aspect_ratio: float,
+                image_width: float) -> rt_camera:
+    """Camera::init (scene.cpp:80-106) via the C-ABI host restatement."""
+    lib = load()
+    cam = rt_camera()
+    check(lib.rt_camera_init(_d3(position), _d3(lookat), _d3(vup), float(vfov),
+                             float(aspect_ratio), float(image_width), C.byref(cam)))
+    return cam
+
+
+def band_rows(height: int, nranks: int, rank: int) -> tuple[int, int]:
+    lib = load()
+    r0, nr = C.c_int32(), C.c_int32()
+    check(lib.rt_band_rows(height, nranks, rank, C.byref(r0), C.byref(nr)))
+    return r0.value, nr.value
+
+
+def out_dtype_shape(out_format: int, nrows: int, width: int):
+    if out_format == RT_OUT_RGB_F32:
+        return np.float32, (nrows, width, 3)
+    if out_format == RT_OUT_RGB_F64:
+        return np.float64, (nrows, width, 3)
+    if out_format == RT_OUT_RGBA8:
+        return np.uint8, (nrows, width, 4)
+    raise ValueError(out_format)
+
+
+class Renderer:
+    """One rt_ctx on one HIP device (the C-ABI's lifecycle, RAII-style)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load()
+        h = C.c_void_p()
+        check(self.lib.rt_ctx_create(int(device), C.byref(h)))
+        self.ctx = h
+        self.device = device
+        self._prims = None
+
+    def close(self):
+        if self.ctx:
+            self.lib.rt_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_scene(self, prims) -> None:
+        arr = (rt_prim * len(prims))(*prims)
+        self._prims = arr
+        check(self.lib.rt_set_scene(self.ctx, arr, len(prims)), self.ctx)
+
+    def render(self, cam: rt_camera, depth: int, precision: int = RT_PREC_F64, flags: int = 0,
+               out_format: int = RT_OUT_RGB_F32, row0: int = 0, nrows: int | None = None,
+               count_segments: bool = False):
+        """Synchronous render into a host numpy array -> (image, stats)."""
+        if nrows is None:
+            nrows = cam.height - row0
+        dt, shape = out_dtype_shape(out_format, nrows, cam.width)
+        out = np.empty(shape, dtype=dt)
+        st = rt_stats()
+        check(self.lib.rt_render(self.ctx, C.byref(cam), row0, nrows, depth, precision, flags,
+                                 out_format, out.ctypes.data_as(C.c_void_p),
+                                 1 if count_segments else 0, C.byref(st)), self.ctx)
+        return out, st
+
+    def render_device(self, cam: rt_camera, depth: int, d_out: int, precision: int = RT_PREC_F64,
+                      flags: int = 0, out_format: int = RT_OUT_RGB_F32, row0: int = 0,
+                      nrows: int | None = None, d_segments: int = 0, stream: int = 0) -> None:
+        """Asynchronous render into device memory `d_out` on `stream` (raw pointers)."""
+        if nrows is None:
+            nrows = cam.height - row0
+        check(self.lib.rt_render_device(self.ctx, C.byref(cam), row0, nrows, depth, precision,
+                                        flags, out_format, C.c_void_p(d_out),
+                                        C.c_void_p(d_segments or None),
+                                        C.c_void_p(stream or None)), self.ctx)

@@ -1,0 +1,112 @@
+"""CPU-side checks of the C-ABI library: it loads, exports every symbol include/*.h
+declares, and its host-only helpers (Camera::init restatement, band partition, format
+sizes, status strings) behave — no device compute is issued here."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+from rtamd import capi, scenes
+
+
+def _declared(header: str):
+    text = open(os.path.join(REPO, "include", header)).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(rt_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = capi.load()
+    declared = _declared("rt_capi.h")
+    assert len(declared) >= 12
+    for name in declared:
+        assert hasattr(lib, name), name
+    bound = {n for n, _, _ in capi.SIGNATURES}
+    assert set(declared) == bound, set(declared) ^ bound
+
+
+def test_nm_dynamic_exports():
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--defined-only", capi.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r" T (rt_[a-z0-9_]+)$", out, flags=re.M))
+    assert set(_declared("rt_capi.h")) <= exported
+
+
+def test_struct_layout_matches_header():
+    assert C.sizeof(capi.rt_material) == 8 * 8
+    assert C.sizeof(capi.rt_prim) == 8 + 64 + 24 + 24 + 24
+    assert C.sizeof(capi.rt_camera) == 12 * 8 + 8
+    assert C.sizeof(capi.rt_stats) == 16
+
+
+def test_camera_init_matches_reference_kat(kat):
+    for c in kat["camera_init"]:
+        a = c["args"]
+        cam = capi.camera_init(a["position"], a["lookat"], a["vup"], a["vfov"], a["aspect_ratio"],
+                               a["image_width"])
+        assert cam.height == c["height"]
+        for field in ("position", "image_top_left", "pixel_delta_x", "pixel_delta_y"):
+            got = np.array(list(getattr(cam, field)))
+            assert np.array_equal(got, np.array(c[field])), (c["name"], field)
+
+
+def test_band_rows_partition():
+    for h in (0, 1, 7, 36, 1080, 4321):
+        for n in (1, 2, 3, 4, 8):
+            rows = []
+            for r in range(n):
+                r0, nr = capi.band_rows(h, n, r)
+                rows.extend(range(r0, r0 + nr))
+            assert rows == list(range(h))
+    with pytest.raises(capi.RTError):
+        capi.band_rows(10, 2, 2)
+
+
+def test_formats_and_status_strings():
+    lib = capi.load()
+    assert lib.rt_out_bytes_per_pixel(capi.RT_OUT_RGB_F32) == 12
+    assert lib.rt_out_bytes_per_pixel(capi.RT_OUT_RGB_F64) == 24
+    assert lib.rt_out_bytes_per_pixel(capi.RT_OUT_RGBA8) == 4
+    assert lib.rt_out_bytes_per_pixel(99) == 0
+    assert lib.rt_strerror(capi.RT_OK) == b"ok"
+    assert lib.rt_strerror(capi.RT_ERR_OUT_OF_RANGE) == b"row band out of range"
+    assert lib.rt_capi_version() == 1
+    assert lib.rt_max_depth() >= 10   # rt_scene's default depth (main.cpp:89)
+
+
+def test_null_args_rejected_without_device():
+    lib = capi.load()
+    assert lib.rt_ctx_create(0, None) == capi.RT_ERR_INVALID_ARG
+    assert lib.rt_ctx_destroy(None) == capi.RT_ERR_INVALID_ARG
+    assert lib.rt_set_scene(None, None, 0) == capi.RT_ERR_INVALID_ARG
+    cam = capi.rt_camera()
+    assert lib.rt_render(None, C.byref(cam), 0, 0, 0, 0, 0, 0, None, 0, None) == \
+        capi.RT_ERR_INVALID_ARG
+    assert lib.rt_camera_init(None, None, None, 90.0, 1.0, 64.0, None) == capi.RT_ERR_INVALID_ARG
+
+
+def test_python_and_c_synthetic_scenes_agree(oracle):
+    for ns, nw in ((8, 4), (64, 6), (256, 0), (0, 6)):
+        c_prims, _ = oracle.synthetic_scene(ns, nw)
+        py_prims = scenes.to_prims(scenes.synthetic_scene(ns, nw))
+        assert len(c_prims) == len(py_prims)
+        for a, b in zip(c_prims, py_prims):
+            assert bytes(a) == bytes(b)
+
+
+def test_default_scene_matches_main_cpp(oracle):
+    arr = (capi.rt_prim * 3)()
+    oracle.lib.orc_default_scene(arr, None)
+    py = scenes.to_prims(scenes.default_scene())
+    for a, b in zip(arr, py):
+        assert bytes(a) == bytes(b)
+
+
+def test_config_cameras():
+    for name, cfg in scenes.CONFIGS.items():
+        cam = capi.camera_init(**scenes.camera_args(cfg.width, cfg.height))
+        assert (cam.width, cam.height) == (cfg.width, cfg.height), name

@@ -1,0 +1,265 @@
+"""GPU parity: the HIP path (through the C-ABI) against the reference's golden frames and
+the oracle, on an MI355X.  Run with `pytest -m gpu`.
+
+Tolerances (north_star: per-pixel RGB delta <= 1e-4 vs the CPU reference):
+  F64    |delta| <= 1e-12 per channel on every pixel of the golden frames (the only
+         difference from the reference is libm's last bit in pow: OCML vs glibc);
+         at full config sizes the same bound on >= 99.999% of pixels, every other pixel
+         on a geometric discontinuity (a 3x3 neighbourhood with differing hit paths).
+  MIXED  bit-identical to F64 (the fp32 cull only skips primitives the exact test rejects).
+  F32    |delta| <= 1e-4 on >= 99.5% of pixels, every outlier on a discontinuity.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import has_gpu, parse_frame_key, scene_by_name
+from rtamd import capi, scenes
+
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(not has_gpu(), reason="needs a HIP device")]
+
+NTHREADS = min(16, len(os.sched_getaffinity(0)))
+
+
+@pytest.fixture(scope="module")
+def rend():
+    r = capi.Renderer(0)
+    yield r
+    r.close()
+
+
+def render(rend, sc, w, h, depth, prec, flags=0, fmt=capi.RT_OUT_RGB_F64, **kw):
+    rend.set_scene(scenes.to_prims(sc))
+    cam = capi.camera_init(**scenes.camera_args(w, h))
+    img, st = rend.render(cam, depth, prec, flags, fmt, **kw)
+    return img, st, cam
+
+
+def discontinuity_mask(sig):
+    """True where any pixel of the 3x3 neighbourhood has a different hit-path signature."""
+    h, w = sig.shape
+    pad = np.pad(sig, 1, mode="edge")
+    m = np.zeros((h, w), bool)
+    for dy in (-1, 0, 1):
+        for dx in (-1, 0, 1):
+            m |= pad[1 + dy:1 + dy + h, 1 + dx:1 + dx + w] != sig
+    return m
+
+
+def check_f64(img, ref64, sig=None, tol=1e-12, min_frac=1.0, what=""):
+    d = np.abs(img - ref64).max(axis=-1)
+    bad = d > tol
+    frac_ok = 1.0 - bad.mean()
+    assert frac_ok >= min_frac, (what, frac_ok, d.max())
+    if bad.any():
+        assert sig is not None, (what, int(bad.sum()), d.max())
+        assert discontinuity_mask(sig)[bad].all(), (what, "outlier off a discontinuity")
+
+
+# ---------------------------------------------------------------- golden frames
+def test_f64_matches_reference_golden_frames(rend, golden_frames):
+    for key in golden_frames.files:
+        name, w, h, depth = parse_frame_key(key)
+        img, _, _ = render(rend, scene_by_name(name), w, h, depth, capi.RT_PREC_F64)
+        check_f64(img, golden_frames[key], what=key)
+
+
+def test_mixed_bitwise_equals_f64_on_golden(rend, golden_frames):
+    for key in golden_frames.files:
+        name, w, h, depth = parse_frame_key(key)
+        a, _, _ = render(rend, scene_by_name(name), w, h, depth, capi.RT_PREC_F64)
+        b, _, _ = render(rend, scene_by_name(name), w, h, depth, capi.RT_PREC_MIXED)
+        assert np.array_equal(a.view(np.uint64), b.view(np.uint64)), key
+
+
+def test_f32_within_tolerance_on_golden(rend, golden_frames, oracle):
+    for key in golden_frames.files:
+        name, w, h, depth = parse_frame_key(key)
+        sc = scene_by_name(name)
+        img, _, cam = render(rend, sc, w, h, depth, capi.RT_PREC_F32, fmt=capi.RT_OUT_RGB_F32)
+        _, _, _, sig = oracle.render(scenes.to_prims(sc), cam, depth, want_sig=True)
+        check_f64(img.astype(np.float64), golden_frames[key], sig, tol=1e-4, min_frac=0.995,
+                  what=key)
+
+
+# ---------------------------------------------------------------- output formats
+def test_f32_output_is_rounded_f64(rend, oracle):
+    sc = scenes.synthetic_scene(8, 4)
+    img32, _, cam = render(rend, sc, 96, 54, 4, capi.RT_PREC_F64, fmt=capi.RT_OUT_RGB_F32)
+    o64, o32, _ = oracle.render(scenes.to_prims(sc), cam, 4)
+    # identical except where a 1e-16 libm difference crosses an fp32 rounding boundary
+    ulp = np.abs(img32.view(np.int32).astype(np.int64) - o32.view(np.int32).astype(np.int64))
+    assert ulp.max() <= 1 and (ulp == 0).mean() > 0.999
+
+
+def test_rgba8_epilogue(rend, oracle):
+    sc = scenes.synthetic_scene(8, 4)
+    img, _, cam = render(rend, sc, 96, 54, 4, capi.RT_PREC_F64, fmt=capi.RT_OUT_RGBA8)
+    o64, _, _ = oracle.render(scenes.to_prims(sc), cam, 4)
+    exp = np.floor(np.clip(o64, 0.0, 1.0) * 255.0).astype(np.uint8)   # main.cpp:345 truncation
+    assert (img[..., 3] == 255).all()
+    edge = np.abs(np.clip(o64, 0, 1) * 255.0 - np.round(np.clip(o64, 0, 1) * 255.0)) < 1e-9
+    ok = (img[..., :3] == exp) | edge
+    assert ok.all()
+
+
+# ---------------------------------------------------------------- semantics
+def test_segment_count_matches_oracle(rend, oracle):
+    for sc, depth in ((scenes.default_scene(), 10), (scenes.synthetic_scene(8, 4), 4),
+                      (scenes.synthetic_scene(64, 6), 6)):
+        for prec in (capi.RT_PREC_F64, capi.RT_PREC_MIXED):
+            _, st, cam = render(rend, sc, 96, 54, depth, prec, count_segments=True)
+            _, _, segs = oracle.render(scenes.to_prims(sc), cam, depth)
+            assert st.segments == segs
+
+
+def test_row_bands_compose_bitwise(rend):
+    sc = scenes.synthetic_scene(8, 4)
+    full, _, cam = render(rend, sc, 100, 75, 4, capi.RT_PREC_F64)
+    parts = []
+    for r0, nr in ((0, 13), (13, 40), (53, 22)):
+        img, _ = rend.render(cam, 4, capi.RT_PREC_F64, 0, capi.RT_OUT_RGB_F64, row0=r0, nrows=nr)
+        parts.append(img)
+    assert np.array_equal(np.concatenate(parts).view(np.uint64), full.view(np.uint64))
+
+
+def test_sun_extension_matches_oracle(rend, oracle):
+    sc = scenes.synthetic_scene(8, 4)
+    for prec in (capi.RT_PREC_F64, capi.RT_PREC_MIXED):
+        img, _, cam = render(rend, sc, 96, 54, 4, prec, flags=capi.RT_FLAG_SUN)
+        o64, _, _ = oracle.render(scenes.to_prims(sc), cam, 4, flags=capi.RT_FLAG_SUN)
+        check_f64(img, o64, what="sun")
+
+
+def test_deterministic(rend):
+    sc = scenes.synthetic_scene(64, 6)
+    a, _, _ = render(rend, sc, 160, 90, 6, capi.RT_PREC_MIXED)
+    b, _, _ = render(rend, sc, 160, 90, 6, capi.RT_PREC_MIXED)
+    assert np.array_equal(a.view(np.uint64), b.view(np.uint64))
+
+
+# ---------------------------------------------------------------- edge cases
+def test_empty_scene_is_sky(rend, oracle):
+    img, _, cam = render(rend, [], 37, 23, 3, capi.RT_PREC_F64)
+    o64, _, _ = oracle.render([], cam, 3)
+    check_f64(img, o64, what="empty")
+
+
+def test_ragged_sizes_and_depths(rend, oracle):
+    sc = scenes.synthetic_scene(5, 3, seed=11)
+    for (w, h) in ((1, 1), (17, 9), (33, 65)):
+        for depth in (0, 1, 5, 9, 16):
+            for prec in (capi.RT_PREC_F64, capi.RT_PREC_MIXED):
+                img, _, cam = render(rend, sc, w, h, depth, prec)
+                o64, _, _, sig = oracle.render(scenes.to_prims(sc), cam, depth, want_sig=True)
+                check_f64(img, o64, sig, what=(w, h, depth, prec))
+
+
+def test_dead_wall_and_degenerate_prims(rend, oracle):
+    # a z-normal wall (NaN basis, never hit: scene.cpp:18) and a zero-radius sphere
+    sc = scenes.synthetic_scene(6, 2, seed=5) + [
+        scenes.Wall(scenes.Material((1, 0, 0)), (-2, -2, 4), (0, 0, 1), 8, 8),
+        scenes.Sphere(scenes.Material((1, 1, 0)), (3, 0, 0), 0.0),
+    ]
+    img, _, cam = render(rend, sc, 64, 36, 4, capi.RT_PREC_F64)
+    o64, _, _, sig = oracle.render(scenes.to_prims(sc), cam, 4, want_sig=True)
+    check_f64(img, o64, sig, what="degenerate")
+
+
+def test_errors(rend):
+    lib = rend.lib
+    cam = capi.camera_init(**scenes.camera_args(64, 36))
+    fresh = capi.Renderer(0)
+    with pytest.raises(capi.RTError) as e:
+        fresh.render(cam, 2)
+    assert e.value.status == capi.RT_ERR_NO_SCENE
+    fresh.close()
+    rend.set_scene(scenes.to_prims(scenes.default_scene()))
+    with pytest.raises(capi.RTError) as e:
+        rend.render(cam, lib.rt_max_depth() + 1)
+    assert e.value.status == capi.RT_ERR_UNSUPPORTED
+    with pytest.raises(capi.RTError) as e:
+        rend.render(cam, 2, row0=30, nrows=10)
+    assert e.value.status == capi.RT_ERR_OUT_OF_RANGE
+
+
+def test_moved_camera_stale_top_left(rend, oracle):
+    """Camera moves without init() (main.cpp:265 -> scene.cpp:121): only position shifts."""
+    sc = scenes.synthetic_scene(8, 4)
+    cam = capi.camera_init(**scenes.camera_args(64, 36))
+    for k in range(3):
+        cam.position[0] += 0.1   # Camera::forward with direction (1,0,0), speed .1
+    rend.set_scene(scenes.to_prims(sc))
+    img, _ = rend.render(cam, 4, capi.RT_PREC_MIXED, 0, capi.RT_OUT_RGB_F64)
+    o64, _, _, sig = oracle.render(scenes.to_prims(sc), cam, 4, want_sig=True)
+    check_f64(img, o64, sig, what="moved")
+
+
+# ---------------------------------------------------------------- mixed-cull stress
+def test_mixed_cull_conservative_random_views(rend):
+    rng = np.random.default_rng(7)
+    for trial in range(6):
+        sc = scenes.synthetic_scene(int(rng.integers(4, 40)), int(rng.integers(0, 7)),
+                                    seed=int(rng.integers(1 << 30)))
+        rend.set_scene(scenes.to_prims(sc))
+        pos = rng.uniform([-1, -3, -1], [6, 3, 2])
+        look = pos + rng.normal(size=3)
+        cam = capi.camera_init(pos, look, (0, 0, -1), float(rng.uniform(30, 120)), 16 / 9, 256.0)
+        depth = int(rng.integers(1, 9))
+        a, _ = rend.render(cam, depth, capi.RT_PREC_F64, 0, capi.RT_OUT_RGB_F64)
+        b, _ = rend.render(cam, depth, capi.RT_PREC_MIXED, 0, capi.RT_OUT_RGB_F64)
+        assert np.array_equal(a.view(np.uint64), b.view(np.uint64)), trial
+
+
+# ---------------------------------------------------------------- full config sizes
+@pytest.mark.parametrize("cfg_name", ["c1", "c2", "c3"])
+def test_full_size_configs_vs_oracle(rend, oracle, cfg_name):
+    cfg = scenes.CONFIGS[cfg_name]
+    sc = cfg.scene()
+    img, st, cam = render(rend, sc, cfg.width, cfg.height, cfg.depth, capi.RT_PREC_MIXED,
+                          count_segments=True)
+    o64, _, segs, sig = oracle.render(scenes.to_prims(sc), cam, cfg.depth, nthreads=NTHREADS,
+                                      want_sig=True)
+    assert st.segments == segs
+    check_f64(img, o64, sig, min_frac=0.99999, what=cfg_name)
+    f32, _, _ = render(rend, sc, cfg.width, cfg.height, cfg.depth, capi.RT_PREC_F32,
+                       fmt=capi.RT_OUT_RGB_F32)
+    check_f64(f32.astype(np.float64), o64, sig, tol=1e-4, min_frac=0.995, what=cfg_name + "/f32")
+
+
+def test_c5_sampled_rows_vs_oracle(rend, oracle):
+    cfg = scenes.CONFIGS["c5"]
+    sc = cfg.scene()
+    rend.set_scene(scenes.to_prims(sc))
+    cam = capi.camera_init(**scenes.camera_args(cfg.width, cfg.height))
+    for r0 in (0, 1500, 2200, 4300):
+        img, st = rend.render(cam, cfg.depth, capi.RT_PREC_MIXED, 0, capi.RT_OUT_RGB_F64,
+                              row0=r0, nrows=8, count_segments=True)
+        o64, _, segs, sig = oracle.render(scenes.to_prims(sc), cam, cfg.depth, row0=r0, nrows=8,
+                                          nthreads=NTHREADS, want_sig=True)
+        assert st.segments == segs
+        check_f64(img, o64, sig, min_frac=0.9999, what=("c5", r0))
+
+
+def test_full_size_c5_properties(rend):
+    """Size-independent properties at BASELINE's largest config: the full 8K frame equals
+    its row bands rendered separately, MIXED equals F64 on a band, values are finite."""
+    cfg = scenes.CONFIGS["c5"]
+    rend.set_scene(scenes.to_prims(cfg.scene()))
+    cam = capi.camera_init(**scenes.camera_args(cfg.width, cfg.height))
+    full, st = rend.render(cam, cfg.depth, capi.RT_PREC_MIXED, 0, capi.RT_OUT_RGB_F32,
+                           count_segments=True)
+    assert np.isfinite(full).all()
+    tot = 0
+    for r in range(4):
+        r0, nr = capi.band_rows(cfg.height, 4, r)
+        b, stb = rend.render(cam, cfg.depth, capi.RT_PREC_MIXED, 0, capi.RT_OUT_RGB_F32,
+                             row0=r0, nrows=nr, count_segments=True)
+        assert np.array_equal(b.view(np.uint32), full[r0:r0 + nr].view(np.uint32))
+        tot += stb.segments
+    assert tot == st.segments
+    a, _ = rend.render(cam, cfg.depth, capi.RT_PREC_F64, 0, capi.RT_OUT_RGB_F32, row0=2000,
+                       nrows=64)
+    assert np.array_equal(a.view(np.uint32), full[2000:2064].view(np.uint32))
