@@ -158,8 +158,15 @@ int32_t rt_out_bytes_per_pixel(int32_t out_format);
  * blocks for multi-GPU tiling: [*row0, *row0 + *nrows). */
 int rt_band_rows(int32_t height, int32_t nranks, int32_t rank, int32_t* row0, int32_t* nrows);
 
-/* Largest depth the kernels are compiled for (depth 0..RT_MAX_DEPTH). */
+/* Largest depth the kernels are compiled for (depth 0..rt_max_depth()). */
 int32_t rt_max_depth(void);
+
+/* ---- diagnostics -------------------------------------------------------- */
+/* Device self-test of the fp64 helpers the exact path relies on, over n seeded random
+ * operands: test 0 = division with a shared refined reciprocal vs IEEE `/` (bitwise),
+ * test 1 = integer-exponent pow by squaring vs pow() (within 128 ulp).
+ * *mismatches receives the number of failures (0 expected). */
+int rt_selftest(rt_ctx* ctx, int32_t test, uint64_t n, uint64_t seed, uint64_t* mismatches);
 
 #ifdef __cplusplus
 }

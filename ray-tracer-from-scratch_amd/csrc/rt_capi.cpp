@@ -24,7 +24,7 @@ struct rt_ctx {
     size_t scene_bytes = 0;
     bool have_scene = false;
     int nS = 0, nW = 0, nP = 0;
-    size_t off_wall = 0, off_mat = 0;
+    size_t off_s64 = 0, off_w32 = 0, off_w64 = 0, off_sj = 0, off_wj = 0, off_mat = 0;
     void* d_out = nullptr;
     size_t d_out_cap = 0;
     unsigned long long* d_segs = nullptr;
@@ -87,12 +87,15 @@ rt::KParams make_params(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, i
                         unsigned long long* d_segs) {
     rt::KParams p{};
     const char* base = static_cast<const char*>(ctx->d_scene);
-    p.sph = reinterpret_cast<const rt::DevSphere*>(base);
-    p.wal = reinterpret_cast<const rt::DevWall*>(base + ctx->off_wall);
+    p.s32 = reinterpret_cast<const rt::SphG32*>(base);
+    p.s64 = reinterpret_cast<const rt::SphG64*>(base + ctx->off_s64);
+    p.w32 = reinterpret_cast<const rt::Wall32*>(base + ctx->off_w32);
+    p.w64 = reinterpret_cast<const rt::Wall64*>(base + ctx->off_w64);
+    p.sph_j = reinterpret_cast<const int32_t*>(base + ctx->off_sj);
+    p.wall_j = reinterpret_cast<const int32_t*>(base + ctx->off_wj);
     p.mat = reinterpret_cast<const rt::DevMat*>(base + ctx->off_mat);
     p.nS = ctx->nS;
     p.nW = ctx->nW;
-    p.nP = ctx->nP;
     p.W = cam->width;
     p.row0 = row0;
     p.nrows = nrows;
@@ -216,44 +219,35 @@ int rt_ctx_create(int device, rt_ctx** out) {
 
 int rt_ctx_destroy(rt_ctx* ctx) {
     if (!ctx) return RT_ERR_INVALID_ARG;
-    hipSetDevice(ctx->device);
-    if (ctx->stream) hipStreamSynchronize(ctx->stream);
-    if (ctx->d_scene) hipFree(ctx->d_scene);
-    if (ctx->d_out) hipFree(ctx->d_out);
-    if (ctx->d_segs) hipFree(ctx->d_segs);
-    if (ctx->ev0) hipEventDestroy(ctx->ev0);
-    if (ctx->ev1) hipEventDestroy(ctx->ev1);
-    if (ctx->stream) hipStreamDestroy(ctx->stream);
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->d_scene) (void)hipFree(ctx->d_scene);
+    if (ctx->d_out) (void)hipFree(ctx->d_out);
+    if (ctx->d_segs) (void)hipFree(ctx->d_segs);
+    if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
+    if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return RT_OK;
 }
 
 int rt_set_scene(rt_ctx* ctx, const rt_prim* prims, int32_t n) {
     if (!ctx || n < 0 || (n > 0 && !prims)) return RT_ERR_INVALID_ARG;
-    std::vector<rt::DevSphere> sph;
-    std::vector<rt::DevWall> wal;
-    std::vector<rt::DevMat> mat((size_t)n);
+    struct Sph {
+        double c[3], r;
+        int32_t j;
+    };
+    struct Wal {
+        double P[3], n[3], X[3], Y[3], len, wid;
+        int32_t j;
+    };
+    std::vector<Sph> sph;
+    std::vector<Wal> wal;
     for (int32_t j = 0; j < n; j++) {
         const rt_prim& q = prims[j];
         if (q.reserved != 0) return RT_ERR_INVALID_ARG;
-        rt::DevMat& m = mat[(size_t)j];
-        for (int k = 0; k < 3; k++) m.color[k] = q.mat.color[k];
-        m.ka = q.mat.ambient;
-        m.km = q.mat.metallic;
-        m.kd = q.mat.diffuse;
-        m.ks = q.mat.specular;
-        m.ex = q.mat.specular_exponent;
         if (q.kind == RT_PRIM_SPHERE) {
-            rt::DevSphere s{};
-            for (int k = 0; k < 3; k++) {
-                s.c[k] = q.position[k];
-                s.cf[k] = (float)q.position[k];
-            }
-            s.r2 = q.radius * q.radius;  // scene.cpp:51
-            s.r2f = (float)s.r2;
-            s.rf = (float)q.radius;
-            s.j = j;
-            sph.push_back(s);
+            sph.push_back(Sph{{q.position[0], q.position[1], q.position[2]}, q.radius, j});
         } else if (q.kind == RT_PRIM_WALL) {
             const hv3 nrm{q.normal[0], q.normal[1], q.normal[2]};
             const hv3 X = hnormalize(hcross(nrm, hv3{0, 0, 1}));  // scene.cpp:18
@@ -261,36 +255,69 @@ int rt_set_scene(rt_ctx* ctx, const rt_prim* prims, int32_t n) {
             // A NaN basis (normal parallel to z) or NaN normal makes every projection NaN:
             // the reference can never report a hit for this wall, so it is not uploaded.
             if (hnan(X) || hnan(Y) || hnan(nrm)) continue;
-            rt::DevWall w{};
-            const double Xa[3] = {X.x, X.y, X.z}, Ya[3] = {Y.x, Y.y, Y.z};
-            for (int k = 0; k < 3; k++) {
-                w.P[k] = q.position[k];
-                w.n[k] = q.normal[k];
-                w.X[k] = Xa[k];
-                w.Y[k] = Ya[k];
-                w.Pf[k] = (float)q.position[k];
-                w.nf[k] = (float)q.normal[k];
-                w.Xf[k] = (float)Xa[k];
-                w.Yf[k] = (float)Ya[k];
-            }
-            w.len = q.length;
-            w.wid = q.width;
-            w.lenf = (float)q.length;
-            w.widf = (float)q.width;
-            w.j = j;
-            wal.push_back(w);
+            wal.push_back(Wal{{q.position[0], q.position[1], q.position[2]},
+                              {nrm.x, nrm.y, nrm.z}, {X.x, X.y, X.z}, {Y.x, Y.y, Y.z},
+                              q.length, q.width, j});
         } else {
             return RT_ERR_INVALID_ARG;
         }
     }
-    const size_t bs = sph.size() * sizeof(rt::DevSphere);
-    const size_t off_wall = align_up(bs, 256);
-    const size_t off_mat = align_up(off_wall + wal.size() * sizeof(rt::DevWall), 256);
-    const size_t total = align_up(off_mat + mat.size() * sizeof(rt::DevMat), 256) + 256;
+    const size_t nS = sph.size(), nW = wal.size(), ng = (nS + 3) / 4;
+    const size_t off_s64 = align_up(ng * sizeof(rt::SphG32), 256);
+    const size_t off_w32 = align_up(off_s64 + ng * sizeof(rt::SphG64), 256);
+    const size_t off_w64 = align_up(off_w32 + nW * sizeof(rt::Wall32), 256);
+    const size_t off_sj = align_up(off_w64 + nW * sizeof(rt::Wall64), 256);
+    const size_t off_wj = align_up(off_sj + nS * sizeof(int32_t), 256);
+    const size_t off_mat = align_up(off_wj + nW * sizeof(int32_t), 256);
+    const size_t total = align_up(off_mat + (nS + nW) * sizeof(rt::DevMat), 256) + 256;
     std::vector<char> host(total, 0);
-    if (!sph.empty()) std::memcpy(host.data(), sph.data(), bs);
-    if (!wal.empty()) std::memcpy(host.data() + off_wall, wal.data(), wal.size() * sizeof(rt::DevWall));
-    if (!mat.empty()) std::memcpy(host.data() + off_mat, mat.data(), mat.size() * sizeof(rt::DevMat));
+    auto* s32 = reinterpret_cast<rt::SphG32*>(host.data());
+    auto* s64 = reinterpret_cast<rt::SphG64*>(host.data() + off_s64);
+    auto* w32 = reinterpret_cast<rt::Wall32*>(host.data() + off_w32);
+    auto* w64 = reinterpret_cast<rt::Wall64*>(host.data() + off_w64);
+    auto* sj = reinterpret_cast<int32_t*>(host.data() + off_sj);
+    auto* wj = reinterpret_cast<int32_t*>(host.data() + off_wj);
+    auto* mat = reinterpret_cast<rt::DevMat*>(host.data() + off_mat);
+    auto put_mat = [&](size_t slot, const rt_material& m) {
+        rt::DevMat& d = mat[slot];
+        for (int k = 0; k < 3; k++) d.color[k] = m.color[k];
+        d.ka = m.ambient;
+        d.km = m.metallic;
+        d.kd = m.diffuse;
+        d.ks = m.specular;
+        d.ex = m.specular_exponent;
+    };
+    for (size_t s = 0; s < nS; s++) {
+        float* f = s32[s / 4].v[s % 4];
+        double* d = s64[s / 4].v[s % 4];
+        for (int k = 0; k < 3; k++) {
+            f[k] = (float)sph[s].c[k];
+            d[k] = sph[s].c[k];
+        }
+        f[3] = (float)sph[s].r;
+        d[3] = sph[s].r * sph[s].r;  // scene.cpp:51
+        sj[s] = sph[s].j;
+        put_mat(s, prims[sph[s].j].mat);
+    }
+    for (size_t w = 0; w < nW; w++) {
+        const Wal& a = wal[w];
+        for (int k = 0; k < 3; k++) {
+            w64[w].P[k] = a.P[k];
+            w64[w].n[k] = a.n[k];
+            w64[w].X[k] = a.X[k];
+            w64[w].Y[k] = a.Y[k];
+            w32[w].P[k] = (float)a.P[k];
+            w32[w].n[k] = (float)a.n[k];
+            w32[w].X[k] = (float)a.X[k];
+            w32[w].Y[k] = (float)a.Y[k];
+        }
+        w64[w].len = a.len;
+        w64[w].wid = a.wid;
+        w32[w].len = (float)a.len;
+        w32[w].wid = (float)a.wid;
+        wj[w] = a.j;
+        put_mat(nS + w, prims[a.j].mat);
+    }
 
     RT_HIP(ctx, hipSetDevice(ctx->device));
     RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -302,12 +329,29 @@ int rt_set_scene(rt_ctx* ctx, const rt_prim* prims, int32_t n) {
         ctx->scene_bytes = total;
     }
     RT_HIP(ctx, hipMemcpy(ctx->d_scene, host.data(), total, hipMemcpyHostToDevice));
-    ctx->nS = (int)sph.size();
-    ctx->nW = (int)wal.size();
+    ctx->nS = (int)nS;
+    ctx->nW = (int)nW;
     ctx->nP = n;
-    ctx->off_wall = off_wall;
+    ctx->off_s64 = off_s64;
+    ctx->off_w32 = off_w32;
+    ctx->off_w64 = off_w64;
+    ctx->off_sj = off_sj;
+    ctx->off_wj = off_wj;
     ctx->off_mat = off_mat;
     ctx->have_scene = true;
+    return RT_OK;
+}
+
+int rt_selftest(rt_ctx* ctx, int32_t test, uint64_t n, uint64_t seed, uint64_t* mismatches) {
+    if (!ctx || !mismatches || test < 0 || test > 1) return RT_ERR_INVALID_ARG;
+    RT_HIP(ctx, hipSetDevice(ctx->device));
+    RT_HIP(ctx, hipMemsetAsync(ctx->d_segs, 0, sizeof(unsigned long long), ctx->stream));
+    const int e = rt::launch_selftest(test, n, seed, ctx->d_segs, ctx->stream);
+    if (e != (int)hipSuccess) return hip_fail(ctx, (hipError_t)e, "launch k_selftest");
+    unsigned long long h = 0;
+    RT_HIP(ctx, hipMemcpyAsync(&h, ctx->d_segs, sizeof h, hipMemcpyDeviceToHost, ctx->stream));
+    RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    *mismatches = h;
     return RT_OK;
 }
 

@@ -1,19 +1,27 @@
 /*
- * rt_device.h — device-side scene records and launch arguments (internal; not ABI).
+ * rt_device.h — device-side scene layout and launch arguments (internal; not ABI).
  *
- * HBM layout of one uploaded scene (one allocation, built by rt_set_scene):
+ * HBM layout of one uploaded scene (one allocation, built by rt_set_scene; every
+ * section 256-B aligned, sphere sections padded to a multiple of 4 records):
  *
- *   [DevSphere x nS][DevWall x nW][DevMat x nP]
+ *   SphG32 [ceil(nS/4)]   4 spheres per 64 B  : {cx, cy, cz, radius}   fp32
+ *   SphG64 [ceil(nS/4)]   4 spheres per 128 B : {cx, cy, cz, radius^2} fp64
+ *   Wall32 [nW]           64 B  : P, n, X, Y, length, width            fp32
+ *   Wall64 [nW]           128 B : P, n, X, Y, length, width            fp64
+ *   int32  sph_j[nS]      scene index of each sphere (tie-break only)
+ *   int32  wall_j[nW]     scene index of each wall (tie-break only)
+ *   DevMat [nS + nW]      64 B, spheres first then walls, indexed by "material slot"
  *
- * Spheres and walls are split by kind so the per-ray scan (find_closest_hit,
- * main.cpp:67-84) runs two branch-free loops instead of a virtual call per primitive;
- * each record keeps its scene index j so ties still resolve to the lowest index as the
- * reference's strict `<` scan does.  Records are wave-uniform (every lane of a wave
- * tests the same primitive), so the kernels read them with scalar loads (one
- * s_load_dwordx16 per sphere) — or broadcast them out of LDS — never per lane.
- * Ray-invariant wall work the reference redoes per test (the basis, scene.cpp:18-19)
- * and r*r (scene.cpp:51) are computed once on the host with the same fp64 operations,
- * so every value is bit-identical to the reference's.
+ * The per-ray scan (find_closest_hit, main.cpp:67-84) runs one loop over sphere groups
+ * and one over walls instead of a virtual call per primitive.  Every lane of a wave tests
+ * the same primitive, so records are wave-uniform: a whole group of 4 spheres arrives
+ * with one s_load_dwordx16 into scalar registers and feeds the VALU as scalar operands
+ * (no LDS traffic, no VGPRs, one scalar-load latency per 4 spheres).  Spheres keep scene
+ * order, so ties between spheres resolve by position in the array; a wall that ties the
+ * current best compares scene indices (strict `<` in scene order == lowest index wins).
+ * Ray-invariant work the reference redoes per test — the wall basis (scene.cpp:18-19)
+ * and radius*radius (scene.cpp:51) — is computed once on the host with the same fp64
+ * operations, so every value is bit-identical to the reference's.
  */
 #ifndef RT_DEVICE_H
 #define RT_DEVICE_H
@@ -22,35 +30,25 @@
 
 namespace rt {
 
-struct alignas(16) DevSphere {  // 64 B
-    double c[3];   // Sphere::center
-    double r2;     // radius * radius (scene.cpp:51, same fp64 product)
-    float cf[3];   // fp32 copies for the F32 path / MIXED cull
-    float r2f;
-    float rf;      // radius (fp32), cull scale
-    int32_t j;     // scene index
-    int32_t pad[2];
+struct alignas(64) SphG32 {
+    float v[4][4];   // [sphere][cx, cy, cz, radius]
 };
-static_assert(sizeof(DevSphere) == 64, "DevSphere layout");
-
-struct alignas(16) DevWall {  // 176 B
-    double P[3];   // Wall::position (corner)
-    double n[3];   // Wall::normal (unit, as the ctor stores it)
-    double X[3];   // normalize(cross(n, (0,0,1)))      scene.cpp:18
-    double Y[3];   // normalize(cross(X, n))             scene.cpp:19
-    double len, wid;
-    float Pf[3], nf[3], Xf[3], Yf[3];
-    float lenf, widf;
-    int32_t j;
-    int32_t pad;
+struct alignas(128) SphG64 {
+    double v[4][4];  // [sphere][cx, cy, cz, radius*radius]
 };
-static_assert(sizeof(DevWall) == 176, "DevWall layout");
-
-struct alignas(16) DevMat {  // 64 B, indexed by scene index
+struct alignas(64) Wall32 {
+    float P[3], n[3], X[3], Y[3], len, wid, pad[2];
+};
+struct alignas(128) Wall64 {
+    double P[3], n[3], X[3], Y[3], len, wid, pad[2];
+};
+struct alignas(64) DevMat {
     double color[3];
     double ka, km, kd, ks, ex;
 };
-static_assert(sizeof(DevMat) == 64, "DevMat layout");
+static_assert(sizeof(SphG32) == 64 && sizeof(SphG64) == 128, "sphere group layout");
+static_assert(sizeof(Wall32) == 64 && sizeof(Wall64) == 128, "wall layout");
+static_assert(sizeof(DevMat) == 64, "material layout");
 
 enum { PREC_F64 = 0, PREC_F32 = 1, PREC_MIXED = 2 };
 enum { OUT_RGB_F32 = 0, OUT_RGB_F64 = 1, OUT_RGBA8 = 2 };
@@ -62,10 +60,14 @@ constexpr int TILE_H = 16;
 constexpr int BLOCK = 256;
 
 struct KParams {
-    const DevSphere* sph;
-    const DevWall* wal;
-    const DevMat* mat;
-    int32_t nS, nW, nP;
+    const SphG32* s32;
+    const SphG64* s64;
+    const Wall32* w32;
+    const Wall64* w64;
+    const int32_t* sph_j;
+    const int32_t* wall_j;
+    const DevMat* mat;     // [nS + nW]
+    int32_t nS, nW;
     int32_t W, row0, nrows, depth;
     uint32_t flags;
     int32_t outf;
@@ -74,9 +76,14 @@ struct KParams {
     unsigned long long* segs;  // may be null
 };
 
-// Host-side launcher (rt_trace.hip).  Returns a hipError_t as int.
+// Host-side launchers (rt_trace.hip).  Return a hipError_t as int.
 int launch_trace(const KParams& p, int prec, void* stream);
 int max_depth();
+// Device self-test of the exact fp64 helpers against IEEE operations:
+// which 0 = division (shared reciprocal), 1 = integer-exponent pow vs pow();
+// adds the number of mismatches (division: bitwise; pow: > 128 ulp) to *d_bad.
+int launch_selftest(int which, uint64_t n, uint64_t seed, unsigned long long* d_bad,
+                    void* stream);
 
 }  // namespace rt
 

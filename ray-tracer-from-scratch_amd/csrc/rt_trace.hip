@@ -8,24 +8,32 @@
  * (vec.cpp:3-57).
  *
  * Precisions (template PREC):
- *   PREC_F64   every operation in fp64, in the reference's order; this TU is built with
- *              -ffp-contract=off so nothing is fused (x86-64 reference codegen has no FMA).
- *              The output matches the reference's fp64 frame up to libm's last-bit
- *              differences in pow (OCML vs glibc).
- *   PREC_F32   fp32 with fused multiply-adds and hardware rcp/rsq/exp/log: the
- *              throughput path; flips at geometric discontinuities (DESIGN.md §parity).
- *   PREC_MIXED fp32 conservative cull in the primitive scan, fp64 exact on every
- *              primitive the cull cannot reject, fp64 shading: output identical to F64.
+ *   PREC_F64   the reference's fp64 arithmetic.  This TU is built with
+ *              -ffp-contract=off, so nothing is fused that the reference (x86-64, no
+ *              FMA) does not fuse; where operations are restructured for speed the
+ *              result is provably bit-identical (see "exact rewrites" below).  The only
+ *              non-bit-exact operations are pow (x^e by squaring for integer e, sky
+ *              z^0.25 as sqrt(sqrt(z))): <= a few ulp, vs glibc's correctly rounded pow.
+ *   PREC_F32   fp32 with fused multiply-adds and hardware rcp/rsq/sqrt/exp/log: the
+ *              throughput path; flips at geometric discontinuities (DESIGN.md).
+ *   PREC_MIXED fp32 conservative cull in the primitive scan, PREC_F64's exact test on
+ *              every primitive the cull cannot reject, fp64 shading: output == F64.
+ *
+ * Exact rewrites (each identity holds in IEEE binary64 barring overflow/underflow):
+ *   - b = 2*dot(d,oc) is exact, so b*b - (4a)*c == 4*(dot*dot - a*c) and
+ *     (-b - sqrt(det)) / (2a) == (-dot - sqrt(det/4)) / a (power-of-two scalings
+ *     commute with rounding; sqrt(4x) == 2*sqrt(x)).
+ *   - x / y for several x and one y: LLVM's fp64 division is rcp + two Newton steps +
+ *     one fma correction wrapped in div_scale/div_fixup, which are identities for
+ *     normal-range operands; sharing the refined reciprocal across numerators gives
+ *     the same bits (checked on device by rt_selftest, tests/test_gpu_parity.py).
+ *   - normalize(-d) == -normalize(d) (negation commutes with rounding).
  *
  * Recursion -> iteration with identical rounding: the reference returns
  * lerp(local, traced, metallic) from the innermost bounce outward (vec.cpp:45-49).
- * Each bounce pushes (shading scalar s, sun scalar, scene index) onto a per-thread
- * register stack indexed by the wave-uniform bounce counter, and the stack is unwound
- * in reverse with the same operations, so local = color*s is recomputed bit-identically.
- *
- * Launch: 256-thread workgroups, 16x16 pixel tiles, each wave an 8x8 square (ray
- * coherence: all 64 lanes test one primitive per iteration, its record read with
- * scalar loads; a primitive no lane can hit costs the wave a skipped branch).
+ * Each bounce pushes (shading scalar s, sun scalar, material slot) onto a per-thread
+ * register stack indexed by the wave-uniform bounce counter; the stack is unwound in
+ * reverse with the same operations, so local = color*s is recomputed bit-identically.
  */
 #include <hip/hip_runtime.h>
 
@@ -48,16 +56,54 @@ __device__ __forceinline__ d3 operator-(d3 a, d3 b) { return D3(a.x - b.x, a.y -
 __device__ __forceinline__ d3 operator-(d3 a) { return D3(-a.x, -a.y, -a.z); }
 __device__ __forceinline__ d3 operator*(d3 a, d3 b) { return D3(a.x * b.x, a.y * b.y, a.z * b.z); }
 __device__ __forceinline__ d3 operator*(d3 a, double s) { return D3(a.x * s, a.y * s, a.z * s); }
-__device__ __forceinline__ d3 operator/(d3 a, double s) { return D3(a.x / s, a.y / s, a.z / s); }
 __device__ __forceinline__ double dot(d3 a, d3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 __device__ __forceinline__ double lensq(d3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
-__device__ __forceinline__ d3 normalize(d3 a) { return a / sqrt(lensq(a)); }
 __device__ __forceinline__ d3 lerp(d3 a, d3 b, double t) {
     return D3(a.x + t * (b.x - a.x), a.y + t * (b.y - a.y), a.z + t * (b.z - a.z));
 }
 __device__ __forceinline__ d3 ld3(const double* p) { return D3(p[0], p[1], p[2]); }
 
-/* fp32 vector math (throughput path) */
+/* Reciprocal refined exactly as LLVM's fp64 division refines it (rcp + 2 Newton). */
+__device__ __forceinline__ double rcp_refined(double b) {
+    double r = __builtin_amdgcn_rcp(b);
+    double e = __builtin_fma(-b, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-b, r, 1.0);
+    return __builtin_fma(r, e, r);
+}
+/* a / b correctly rounded, given r = rcp_refined(b) (a == 0 keeps IEEE's signed zero). */
+__device__ __forceinline__ double div_r(double a, double b, double r) {
+    const double q = a * r;
+    const double e = __builtin_fma(-b, q, a);
+    const double q1 = __builtin_fma(e, r, q);
+    return a == 0.0 ? q : q1;
+}
+/* v / len(v) component-wise (vec.cpp:21), one shared reciprocal. */
+__device__ __forceinline__ d3 normalize_e(d3 v) {
+    const double l = sqrt(lensq(v));
+    const double r = rcp_refined(l);
+    return D3(div_r(v.x, l, r), div_r(v.y, l, r), div_r(v.z, l, r));
+}
+__device__ __forceinline__ d3 div3(d3 v, double l, double r) {
+    return D3(div_r(v.x, l, r), div_r(v.y, l, r), div_r(v.z, l, r));
+}
+/* x^e for x >= 0: binary powering when e is a small non-negative integer (every
+ * material in the reference and the configs: 30, 50), else pow(). */
+__device__ __forceinline__ double pow_e(double x, double e) {
+    if (e >= 0.0 && e <= 1024.0 && e == __builtin_rint(e)) {
+        int n = (int)e;
+        double acc = 1.0, b = x;
+        while (n) {
+            if (n & 1) acc *= b;
+            n >>= 1;
+            if (n) b *= b;
+        }
+        return acc;
+    }
+    return pow(x, e);
+}
+
+/* fp32 vector math (throughput path; FMAs explicit) */
 struct f3 {
     float x, y, z;
 };
@@ -69,11 +115,14 @@ __device__ __forceinline__ f3 operator*(f3 a, float s) { return F3(a.x * s, a.y 
 __device__ __forceinline__ float fdot(f3 a, f3 b) { return fmaf(a.x, b.x, fmaf(a.y, b.y, a.z * b.z)); }
 __device__ __forceinline__ float frsq(float x) { return __builtin_amdgcn_rsqf(x); }
 __device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ float fsqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
 __device__ __forceinline__ f3 fnormalize(f3 a) { return a * frsq(fdot(a, a)); }
 __device__ __forceinline__ f3 fmad3(f3 a, float s, f3 b) {  // a*s + b
     return F3(fmaf(a.x, s, b.x), fmaf(a.y, s, b.y), fmaf(a.z, s, b.z));
 }
-__device__ __forceinline__ f3 ld3f(const float* p) { return F3(p[0], p[1], p[2]); }
+__device__ __forceinline__ float fmax3abs(float a, float b, float c) {
+    return fmaxf(fmaxf(fabsf(a), fabsf(b)), fabsf(c));
+}
 /* x^e for x >= 0 via v_log_f32 / v_exp_f32 (pow(0,e>0) = 0, pow(x,0) = 1). */
 __device__ __forceinline__ float fpow(float x, float e) {
     if (e == 0.0f) return 1.0f;
@@ -81,216 +130,219 @@ __device__ __forceinline__ float fpow(float x, float e) {
 }
 
 /* main.cpp:14-19 */
-#define LIGHT_X 0.0
-#define LIGHT_Y 0.0
-#define LIGHT_Z 0.0
 __device__ __forceinline__ d3 ground_color() { return D3(0.025, 0.05, 0.075); }
 __device__ __forceinline__ d3 sky_low() { return D3(0.36, 0.45, 0.57); }
 __device__ __forceinline__ d3 sky_high() { return D3(0.14, 0.21, 0.49); }
 __device__ __forceinline__ d3 sun_color() { return D3(1.64, 1.27, 0.99); }
 __device__ __forceinline__ d3 sun_direction() { return D3(.7, .4, .7); }
 
-/* Largest bounce count compiled: the stack is sized per instantiation. */
+/* Largest bounce count compiled: the register stack is sized per instantiation. */
 constexpr int MAXD_SMALL = 4;
 constexpr int MAXD_MID = 8;
 constexpr int MAXD_LARGE = 16;
 
 /* ------------------------------------------------------------------------ */
-/* fp64 closest hit (find_closest_hit, main.cpp:67-84)                       */
+/* closest hit (find_closest_hit, main.cpp:67-84)                            */
 /* ------------------------------------------------------------------------ */
+/* Winner of the scan.  The reference's strict `0 < d < best` scan in scene order returns
+ * the lowest scene index among the minimum distance; spheres are visited in scene order
+ * (ties among them keep the earlier one) and a wall that ties the best compares scene
+ * indices, so the winner is the same. */
 struct HitD {
     double dist;  // the value find_closest_hit compares (sphere: world, wall: parametric)
-    double pt;    // sphere: the parameter of the intersection point used for the normal
-    int j;        // scene index, -1 = miss
-    int slot;     // index into the sphere or wall array
-    bool sphere;
+    double pt;    // sphere: parameter of the intersection point used for the normal
+    int slot;     // material slot: sphere s -> s, wall w -> nS + w; -1 = miss
 };
 
-/* Accept rule of main.cpp:77 in an order-independent form: the reference's strict
- * `0 < d < best` scan in scene order returns the lowest j among the minimum d, so any
- * visiting order gives the same winner with ties broken on j. */
-__device__ __forceinline__ bool better(double dist, int j, const HitD& h) {
-    return dist > 0 && (dist < h.dist || (dist == h.dist && j < h.j));
-}
+struct RayD {
+    d3 o, d;
+    double a;     // |d|^2
+    double ra;    // rcp_refined(a)
+    double dlen;  // sqrt(a) == d.length()
+};
 
-/* Sphere::intersect (scene.cpp:40-78), exact.  Only the branches that can produce an
- * accepted distance are evaluated; every skip is exact:
- *   det < 0                 -> miss (scene.cpp:57)
- *   b > 0                   -> proj = (-b - sqrt(det)) / (2a) < 0, rejected by d > 0
- *   -b - sqrt(det) <= 0     -> proj <= 0 (or NaN), rejected
- * and p1 is never the minimum: (-b+sq)/(2a) >= (-b-sq)/(2a) by monotonic rounding. */
-__device__ __forceinline__ void sphere_test_d(const DevSphere& S, const d3 o, const d3 d,
-                                              const double a, const double two_a,
-                                              const double four_a, const double dlen, int s,
-                                              HitD& h) {
-    const d3 oc = o - D3(S.c[0], S.c[1], S.c[2]);
-    const double b = 2 * dot(d, oc);
-    if (b > 0) return;
-    const double c = lensq(oc) - S.r2;
-    const double det = b * b - four_a * c;
-    if (!(det >= 0)) return;
+/* Sphere::intersect (scene.cpp:40-78), exact, in the scaled form (file header).  Only
+ * branches that can produce an accepted distance are evaluated; every skip is exact:
+ *   dot > 0 (b > 0)    -> proj = (-b - sqrt(det)) / 2a < 0, rejected by d > 0
+ *   x < 0 (det < 0)    -> miss (scene.cpp:57)
+ *   -dot - sqrt(x) <= 0 -> proj <= 0, rejected
+ * and p1 is never the minimum: (-b+sq)/2a >= (-b-sq)/2a by monotonic rounding. */
+__device__ __forceinline__ void sphere_exact(const double* S, int s, const RayD& r, HitD& h) {
+    const d3 oc = r.o - D3(S[0], S[1], S[2]);
+    const double dt = dot(r.d, oc);  // b / 2
+    if (dt > 0) return;
+    const double c = lensq(oc) - S[3];
+    const double x = dt * dt - r.a * c;  // det / 4
+    if (!(x >= 0)) return;
     double proj, pt;
-    if (det == 0) {
-        pt = -b / two_a;
-        proj = (-b - sqrt(det)) / a;  // scene.cpp:65 (/a, not /2a) kept
+    if (x == 0) {
+        pt = div_r(-dt, r.a, r.ra);  // -b / (2a)
+        proj = 2.0 * pt;             // (-b - sqrt(0)) / a: scene.cpp:65's /a kept
     } else {
-        const double num = -b - sqrt(det);
+        const double num = -dt - sqrt(x);
         if (!(num > 0)) return;
-        proj = num / two_a;
+        proj = div_r(num, r.a, r.ra);
         pt = proj;
     }
-    const double dist = proj * dlen;  // world distance, scene.cpp:77
-    if (better(dist, S.j, h)) {
+    const double dist = proj * r.dlen;  // world distance, scene.cpp:77
+    if (dist > 0 && dist < h.dist) {
         h.dist = dist;
         h.pt = pt;
-        h.j = S.j;
         h.slot = s;
-        h.sphere = true;
     }
 }
 
-/* Wall::intersect (scene.cpp:4-35), exact.  t = num/denom is formed only when the
- * signs make t > 0 possible (denom == 0 or NaN can never pass the bounds check). */
-__device__ __forceinline__ void wall_test_d(const DevWall& Wl, const d3 o, const d3 d, int w,
-                                            HitD& h) {
-    const d3 n = D3(Wl.n[0], Wl.n[1], Wl.n[2]);
-    const d3 P = D3(Wl.P[0], Wl.P[1], Wl.P[2]);
-    const double denom = dot(n, d);
-    const double num = dot(P - o, n);
-    if (!((num > 0 && denom > 0) || (num < 0 && denom < 0))) return;
-    const double t = num / denom;
+__device__ __forceinline__ int scene_index(const KParams& p, int slot) {
+    return slot < p.nS ? p.sph_j[slot] : p.wall_j[slot - p.nS];
+}
+
+/* Wall::intersect (scene.cpp:4-35), exact.  t = num/denom is formed only when the signs
+ * make t > 0 possible (denom == 0 or NaN can never pass the bounds check). */
+__device__ __forceinline__ void wall_exact(const Wall64& Wl, int w, const KParams& p,
+                                           const RayD& r, HitD& h) {
+    const d3 n = ld3(Wl.n);
+    const d3 P = ld3(Wl.P);
+    const double den = dot(n, r.d);
+    const double num = dot(P - r.o, n);
+    if (!((num > 0 && den > 0) || (num < 0 && den < 0))) return;
+    const double t = div_r(num, den, rcp_refined(den));
     if (!(t > 0)) return;
-    const d3 ip = o + d * t;  // ray::at, scene.h:16
-    const d3 q = ip - P;
-    const double px = dot(q, D3(Wl.X[0], Wl.X[1], Wl.X[2]));
-    const double py = dot(q, D3(Wl.Y[0], Wl.Y[1], Wl.Y[2]));
+    const d3 q = (r.o + r.d * t) - P;  // ray::at (scene.h:16) minus the corner
+    const double px = dot(q, ld3(Wl.X));
+    const double py = dot(q, ld3(Wl.Y));
     if (px >= 0 && px <= Wl.len && py >= 0 && py <= Wl.wid) {
-        if (better(t, Wl.j, h)) {  // parametric t compared as-is (main.cpp:77)
+        bool take = t < h.dist;
+        if (!take && t == h.dist && h.slot >= 0)  // tie: the lower scene index wins (rare)
+            take = p.wall_j[w] < scene_index(p, h.slot);
+        if (take) {
             h.dist = t;
-            h.j = Wl.j;
-            h.slot = w;
-            h.sphere = false;
+            h.slot = p.nS + w;
         }
     }
 }
 
 /* MIXED: fp32 conservative cull in front of the exact sphere test.  A sphere is skipped
  * only when the fp32 evaluation proves, with a margin covering its rounding error, that
- * the exact test would reject it (det < 0, or b > 0).  See DESIGN.md §mixed. */
+ * the exact test rejects it (det < 0, or b > 0).  Margins:
+ *   |b/2 error| <= 18u*dinf*B,  |det/4 error| <= 133u*a*B^2 + ...,  B = |o|inf+|C|inf+r,
+ * bounded here by K*dinf*B and 8K*a*B^2 with K = 512u. */
 struct RayF {
     f3 o, d;
-    float a;      // |d|^2
-    float dinf;   // max |d_i|
-    float oinf;   // max |o_i|
+    float a;
+    float kb;     // K * dinf
+    float kdet;   // 8K * a
+    float oinf;
 };
 constexpr float CULL_U = 1.0f / 16777216.0f;  // 2^-24
-constexpr float CULL_K = 512.0f * CULL_U;     // generous multiple of the unit roundoff
+constexpr float CULL_K = 512.0f * CULL_U;
 
-__device__ __forceinline__ bool sphere_cull_f(const DevSphere& S, const RayF& r) {
-    const f3 oc = r.o - F3(S.cf[0], S.cf[1], S.cf[2]);
-    const float bh = fdot(r.d, oc);                // b/2
-    const float c = fmaf(-S.rf, S.rf, fdot(oc, oc));
-    const float det = fmaf(bh, bh, -r.a * c);       // det/4
-    const float B = r.oinf + fmaxf(fmaxf(fabsf(S.cf[0]), fabsf(S.cf[1])), fabsf(S.cf[2])) + S.rf;
-    const float mb = CULL_K * r.dinf * B;
-    const float mdet = CULL_K * (r.a * B * B + bh * bh + r.a * fabsf(c));
-    return (bh > mb) || (det < -mdet);
+__device__ __forceinline__ bool sphere_cull(const float* S, const RayF& r) {
+    const f3 oc = r.o - F3(S[0], S[1], S[2]);
+    const float bh = fdot(r.d, oc);
+    const float c = fmaf(-S[3], S[3], fdot(oc, oc));
+    const float det = fmaf(bh, bh, -r.a * c);
+    const float B = r.oinf + fmax3abs(S[0], S[1], S[2]) + S[3];
+    return (bh > r.kb * B) || (det < -r.kdet * (B * B));
 }
 
-__device__ __forceinline__ bool wall_cull_f(const DevWall& Wl, const RayF& r) {
-    const f3 n = ld3f(Wl.nf), P = ld3f(Wl.Pf);
-    const f3 po = P - r.o;
+__device__ __forceinline__ bool wall_cull(const Wall32& Wl, const RayF& r) {
+    const f3 n = F3(Wl.n[0], Wl.n[1], Wl.n[2]), P = F3(Wl.P[0], Wl.P[1], Wl.P[2]);
     const float den = fdot(n, r.d);
-    const float num = fdot(po, n);
-    const float B = r.oinf + fmaxf(fmaxf(fabsf(P.x), fabsf(P.y)), fabsf(P.z));
+    const float num = fdot(P - r.o, n);
+    const float B = r.oinf + fmax3abs(P.x, P.y, P.z);
     const float mnum = CULL_K * B;
-    const float mden = CULL_K * r.dinf;
+    const float mden = r.kb;
     if ((num < -mnum && den > mden) || (num > mnum && den < -mden)) return true;  // t < 0
     if (fabsf(num) <= 64.0f * mnum || fabsf(den) <= 64.0f * mden) return false;   // ill-conditioned
     // t's relative error <= mnum/|num| + mden/|den| (<= 1/32 here); bound the point error.
     const float t = num * frcp(den);
     const float rel = mnum / fabsf(num) + mden / fabsf(den) + 4.0f * CULL_U;
     const f3 q = fmad3(r.d, t, r.o) - P;
-    const float len_dt = sqrtf(r.a) * fabsf(t);
-    const float err = 2.0f * len_dt * rel + CULL_K * (B + len_dt + Wl.lenf + Wl.widf);
-    const float px = fdot(q, ld3f(Wl.Xf));
-    const float py = fdot(q, ld3f(Wl.Yf));
-    return px < -err || px > Wl.lenf + err || py < -err || py > Wl.widf + err;
+    const float len_dt = fsqrt(r.a) * fabsf(t);
+    const float err = 2.0f * len_dt * rel + CULL_K * (B + len_dt + Wl.len + Wl.wid);
+    const float px = fdot(q, F3(Wl.X[0], Wl.X[1], Wl.X[2]));
+    const float py = fdot(q, F3(Wl.Y[0], Wl.Y[1], Wl.Y[2]));
+    return px < -err || px > Wl.len + err || py < -err || py > Wl.wid + err;
 }
 
 template <bool MIXED>
-__device__ __forceinline__ HitD closest_hit_d(const KParams& p, const d3 o, const d3 d,
-                                              const double a, const double dlen) {
+__device__ __forceinline__ HitD closest_hit_d(const KParams& p, const RayD& r) {
     HitD h;
     h.dist = DBL_MAX;
     h.pt = 0;
-    h.j = -1;
-    h.slot = 0;
-    h.sphere = false;
-    const double two_a = 2 * a, four_a = 4 * a;
+    h.slot = -1;
     RayF rf;
     if (MIXED) {
-        rf.o = F3((float)o.x, (float)o.y, (float)o.z);
-        rf.d = F3((float)d.x, (float)d.y, (float)d.z);
+        rf.o = F3((float)r.o.x, (float)r.o.y, (float)r.o.z);
+        rf.d = F3((float)r.d.x, (float)r.d.y, (float)r.d.z);
         rf.a = fdot(rf.d, rf.d);
-        rf.dinf = fmaxf(fmaxf(fabsf(rf.d.x), fabsf(rf.d.y)), fabsf(rf.d.z));
-        rf.oinf = fmaxf(fmaxf(fabsf(rf.o.x), fabsf(rf.o.y)), fabsf(rf.o.z));
+        rf.kb = CULL_K * fmax3abs(rf.d.x, rf.d.y, rf.d.z);
+        rf.kdet = 8.0f * CULL_K * rf.a;
+        rf.oinf = fmax3abs(rf.o.x, rf.o.y, rf.o.z);
     }
-    for (int s = 0; s < p.nS; ++s) {
-        const DevSphere& S = p.sph[s];
-        if (MIXED && sphere_cull_f(S, rf)) continue;
-        sphere_test_d(S, o, d, a, two_a, four_a, dlen, s, h);
+    const int ng = (p.nS + 3) >> 2;
+    for (int g = 0; g < ng; ++g) {
+        if (MIXED) {
+            const SphG32 G = p.s32[g];  // one s_load_dwordx16
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int s = 4 * g + k;
+                if (s < p.nS && !sphere_cull(G.v[k], rf)) sphere_exact(p.s64[g].v[k], s, r, h);
+            }
+        } else {
+            const SphG64 G = p.s64[g];  // two s_load_dwordx16
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int s = 4 * g + k;
+                if (s < p.nS) sphere_exact(G.v[k], s, r, h);
+            }
+        }
     }
     for (int w = 0; w < p.nW; ++w) {
-        const DevWall& Wl = p.wal[w];
-        if (MIXED && wall_cull_f(Wl, rf)) continue;
-        wall_test_d(Wl, o, d, w, h);
+        if (MIXED && wall_cull(p.w32[w], rf)) continue;
+        wall_exact(p.w64[w], w, p, r, h);
     }
     return h;
 }
 
-/* out_color, main.cpp:28-37 (float skyGradient 0.25f promoted to double). */
-__device__ __forceinline__ d3 out_color_d(d3 v) {
-    if (v.z < 0.0) return ground_color();
-    v = normalize(v);
-    return lerp(sky_low(), sky_high(), pow(v.z, (double)0.25f));
+/* out_color, main.cpp:28-37: only normalize(v).z is used; z^0.25 as sqrt(sqrt(z)). */
+__device__ __forceinline__ d3 sky_d(const RayD& r, double nvz) {
+    if (r.d.z < 0.0) return ground_color();
+    return lerp(sky_low(), sky_high(), sqrt(sqrt(nvz)));
 }
 
 /* Shading of one hit (main.cpp:99-104 + diffuse_shading + specular), returning
- * s = diffuse*kd + spec*ks + ka (local = color * s), the unit normal and the
- * (optional) sun scalar.  Shared normalisations are computed once: they are the same
- * operations on the same operands as the reference's repeated calls. */
+ * s = diffuse*kd + spec*ks + ka (local = color * s) and the (optional) sun scalar.
+ * Shared normalisations are computed once: the same operations on the same operands
+ * as the reference's repeated calls. */
 struct ShadeD {
     double s;
     double ksun;
 };
-__device__ __forceinline__ ShadeD shade_d(const DevMat& m, const d3 pos, const d3 N, const d3 view,
-                                          bool sun) {
-    const d3 lv = D3(LIGHT_X - pos.x, LIGHT_Y - pos.y, LIGHT_Z - pos.z);
-    const d3 ldir = normalize(lv);
-    const d3 nn = normalize(N);
+__device__ __forceinline__ ShadeD shade_d(const DevMat& m, const d3 pos, const d3 nn,
+                                          const d3 view, bool sun) {
+    const d3 ldir = normalize_e(D3(0.0 - pos.x, 0.0 - pos.y, 0.0 - pos.z));  // LIGHT_POS - pos
     const double lamb = dot(ldir, nn);
     const double diffuse = lamb > 0 ? lamb : 0;
-    const d3 halfway = normalize(view + ldir);
-    double res = dot(halfway, nn);
+    double res = dot(normalize_e(view + ldir), nn);
     res = res > 0 ? res : 0;
-    const double spec = pow(res, m.ex);
-    ShadeD r;
-    r.s = diffuse * m.kd + spec * m.ks + m.ka;
-    r.ksun = 0;
+    const double spec = pow_e(res, m.ex);
+    ShadeD sh;
+    sh.s = diffuse * m.kd + spec * m.ks + m.ka;
+    sh.ksun = 0;
     if (sun) {  // build-defined (rt_oracle.c sun_term)
-        const d3 sd = normalize(sun_direction());
+        const d3 sd = normalize_e(sun_direction());
         double a = dot(sd, nn);
         a = a > 0 ? a : 0;
-        double hs = dot(normalize(view + sd), nn);
+        double hs = dot(normalize_e(view + sd), nn);
         hs = hs > 0 ? hs : 0;
-        r.ksun = a * m.kd + pow(hs, m.ex) * m.ks;
+        sh.ksun = a * m.kd + pow_e(hs, m.ex) * m.ks;
     }
-    return r;
+    return sh;
 }
 
-/* local = color * s (+ (SUN_COLOR * color) * ksun) — identical operations at push
- * and at unwind. */
+/* local = color * s (+ (SUN_COLOR * color) * ksun): identical operations at push and at
+ * unwind. */
 __device__ __forceinline__ d3 local_color_d(const DevMat& m, double s, double ksun, bool sun) {
     const d3 col = ld3(m.color);
     d3 L = col * s;
@@ -298,57 +350,63 @@ __device__ __forceinline__ d3 local_color_d(const DevMat& m, double s, double ks
     return L;
 }
 
+__device__ __forceinline__ RayD make_ray(d3 o, d3 d) {
+    RayD r;
+    r.o = o;
+    r.d = d;
+    r.a = lensq(d);
+    r.ra = rcp_refined(r.a);
+    r.dlen = sqrt(r.a);
+    return r;
+}
+
 template <bool MIXED, int MAXD>
 __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, int& segs) {
     const d3 cpos = ld3(p.pos);
     const d3 pc = (ld3(p.tl) + ld3(p.dx) * (double)x) + ld3(p.dy) * (double)i;  // main.cpp:132
-    d3 o = cpos;
-    d3 d = cpos - pc;  // main.cpp:133 (not normalised)
+    RayD r = make_ray(cpos, cpos - pc);  // main.cpp:133-134 (direction not normalised)
     const bool sun = (p.flags & FLAG_SUN) != 0;
 
     double st_s[MAXD];
     double st_k[MAXD];
-    int st_j[MAXD];
+    int st_m[MAXD];
     int n = 0;
     d3 c;
     for (int k = 0;; ++k) {
         ++segs;
-        const double a = lensq(d);
-        const double dlen = sqrt(a);
-        const HitD h = closest_hit_d<MIXED>(p, o, d, a, dlen);
-        if (h.j < 0) {
-            c = out_color_d(d);
+        const HitD h = closest_hit_d<MIXED>(p, r);
+        const double rdl = rcp_refined(r.dlen);
+        const d3 nv = div3(r.d, r.dlen, rdl);  // normalize(d); normalize(-d) == -nv
+        if (h.slot < 0) {
+            c = sky_d(r, nv.z);
             break;
         }
-        const d3 pos = o + d * h.dist;  // main.cpp:99 (sphere world distance used as t)
+        const d3 pos = r.o + r.d * h.dist;  // main.cpp:99 (sphere world distance used as t)
         d3 N;
-        if (h.sphere) {
-            const DevSphere& S = p.sph[h.slot];
-            N = (o + d * h.pt) - D3(S.c[0], S.c[1], S.c[2]);  // un-normalised, length r
+        if (h.slot < p.nS) {
+            const double* S = p.s64[h.slot >> 2].v[h.slot & 3];
+            N = (r.o + r.d * h.pt) - D3(S[0], S[1], S[2]);  // un-normalised, length r
         } else {
-            const DevWall& Wl = p.wal[h.slot];
-            N = D3(Wl.n[0], Wl.n[1], Wl.n[2]);
+            N = ld3(p.w64[h.slot - p.nS].n);
         }
-        const DevMat& m = p.mat[h.j];
-        const d3 nv = d / dlen;  // normalize(d) == -normalize(-d) bit for bit
-        const ShadeD sh = shade_d(m, pos, N, -nv, sun);
+        const DevMat& m = p.mat[h.slot];
+        const d3 nn = normalize_e(N);
+        const ShadeD sh = shade_d(m, pos, nn, -nv, sun);
         if (k >= p.depth || k >= MAXD) {  // remaining_iterations <= 0 (main.cpp:105)
             c = local_color_d(m, sh.s, sh.ksun, sun);
             break;
         }
         st_s[k] = sh.s;
         st_k[k] = sh.ksun;
-        st_j[k] = h.j;
+        st_m[k] = h.slot;
         n = k + 1;
-        // reflect(d, N) (vec.cpp:51-57) and the offset start (main.cpp:111-113)
-        const d3 nn = normalize(N);
+        // start + reflect(d, N) (main.cpp:111-113, vec.cpp:51-57)
         const double cc = 2 * dot(nv, nn);
-        o = pos + N * .0001;
-        d = nv - nn * cc;
+        r = make_ray(pos + N * .0001, nv - nn * cc);
     }
     for (int q = MAXD - 1; q >= 0; --q) {
         if (q < n) {
-            const DevMat& m = p.mat[st_j[q]];
+            const DevMat& m = p.mat[st_m[q]];
             const d3 L = local_color_d(m, st_s[q], st_k[q], sun);
             c = lerp(L, c, m.km);  // vec.cpp:45-49 via main.cpp:117
         }
@@ -359,103 +417,96 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, int&
 /* ------------------------------------------------------------------------ */
 /* fp32 throughput path                                                      */
 /* ------------------------------------------------------------------------ */
-struct HitF {
-    float dist, pt;
-    int j, slot;
-    bool sphere;
-};
-
 template <int MAXD>
 __device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, int& segs) {
-    const f3 cpos = F3((float)p.pos[0], (float)p.pos[1], (float)p.pos[2]);
-    // ray generation in fp64 (cheap, once per pixel) then rounded
     const d3 pcd = (ld3(p.tl) + ld3(p.dx) * (double)x) + ld3(p.dy) * (double)i;
     const d3 dd = ld3(p.pos) - pcd;
-    f3 o = cpos;
+    f3 o = F3((float)p.pos[0], (float)p.pos[1], (float)p.pos[2]);
     f3 d = F3((float)dd.x, (float)dd.y, (float)dd.z);
     const bool sun = (p.flags & FLAG_SUN) != 0;
 
     float st_s[MAXD];
     float st_k[MAXD];
-    int st_j[MAXD];
+    int st_m[MAXD];
     int n = 0;
     f3 c;
     for (int k = 0;; ++k) {
         ++segs;
         const float a = fdot(d, d);
-        const float inv_a = frcp(a);
-        const float dlen = sqrtf(a);
-        HitF h;
-        h.dist = FLT_MAX;
-        h.pt = 0;
-        h.j = -1;
-        h.slot = 0;
-        h.sphere = false;
-        for (int s = 0; s < p.nS; ++s) {
-            const DevSphere& S = p.sph[s];
-            const f3 oc = o - ld3f(S.cf);
-            const float bh = fdot(d, oc);
-            if (bh > 0) continue;
-            const float cq = fdot(oc, oc) - S.r2f;
-            const float det = fmaf(bh, bh, -a * cq);
-            if (!(det >= 0)) continue;
-            float proj, pt;
-            if (det == 0) {
-                pt = -bh * inv_a;
-                proj = 2.0f * pt;  // scene.cpp:65 quirk: -b/a = 2 * (-b/2a)
-            } else {
-                const float num = -bh - sqrtf(det);
-                if (!(num > 0)) continue;
-                proj = num * inv_a;
-                pt = proj;
-            }
-            const float dist = proj * dlen;
-            if (dist > 0 && (dist < h.dist || (dist == h.dist && S.j < h.j))) {
-                h.dist = dist; h.pt = pt; h.j = S.j; h.slot = s; h.sphere = true;
+        const float ra = frcp(a);
+        const float rl = frsq(a);
+        float best = FLT_MAX, bpt = 0.0f;
+        int slot = -1;
+        const int ng = (p.nS + 3) >> 2;
+        for (int g = 0; g < ng; ++g) {
+            const SphG32 G = p.s32[g];
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {
+                const int s = 4 * g + kk;
+                if (s >= p.nS) break;
+                const float* S = G.v[kk];
+                const f3 oc = o - F3(S[0], S[1], S[2]);
+                const float bh = fdot(d, oc);
+                const float cq = fmaf(-S[3], S[3], fdot(oc, oc));
+                const float det = fmaf(bh, bh, -a * cq);
+                const float num = -bh - fsqrt(fmaxf(det, 0.0f));
+                // b <= 0, det >= 0, positive root; det==0 keeps scene.cpp:65's 2x
+                float proj = num * ra;
+                proj = (det == 0.0f) ? -2.0f * bh * ra : proj;
+                const float dist = proj * a * rl;  // proj * |d|
+                if (bh <= 0.0f && det >= 0.0f && num > 0.0f && dist > 0.0f && dist < best) {
+                    best = dist;
+                    bpt = (det == 0.0f) ? -bh * ra : proj;
+                    slot = s;
+                }
             }
         }
         for (int w = 0; w < p.nW; ++w) {
-            const DevWall& Wl = p.wal[w];
-            const f3 nw = ld3f(Wl.nf), P = ld3f(Wl.Pf);
+            const Wall32& Wl = p.w32[w];
+            const f3 nw = F3(Wl.n[0], Wl.n[1], Wl.n[2]), P = F3(Wl.P[0], Wl.P[1], Wl.P[2]);
             const float den = fdot(nw, d);
             const float num = fdot(P - o, nw);
             if (!((num > 0 && den > 0) || (num < 0 && den < 0))) continue;
-            const float t = num / den;
-            if (!(t > 0)) continue;
+            const float t = num * frcp(den);
             const f3 q = fmad3(d, t, o) - P;
-            const float px = fdot(q, ld3f(Wl.Xf));
-            const float py = fdot(q, ld3f(Wl.Yf));
-            if (px >= 0 && px <= Wl.lenf && py >= 0 && py <= Wl.widf &&
-                (t < h.dist || (t == h.dist && Wl.j < h.j))) {
-                h.dist = t; h.j = Wl.j; h.slot = w; h.sphere = false;
+            const float px = fdot(q, F3(Wl.X[0], Wl.X[1], Wl.X[2]));
+            const float py = fdot(q, F3(Wl.Y[0], Wl.Y[1], Wl.Y[2]));
+            if (t > 0 && px >= 0 && px <= Wl.len && py >= 0 && py <= Wl.wid) {
+                bool take = t < best;
+                if (!take && t == best && slot >= 0) take = p.wall_j[w] < scene_index(p, slot);
+                if (take) {
+                    best = t;
+                    slot = p.nS + w;
+                }
             }
         }
-        if (h.j < 0) {
+        const f3 nv = d * rl;
+        if (slot < 0) {
             if (d.z < 0.0f) {
                 c = F3(0.025f, 0.05f, 0.075f);
             } else {
-                const float z = d.z * frsq(a);
-                const float tz = sqrtf(sqrtf(z));
+                const float tz = fsqrt(fsqrt(nv.z));
                 c = F3(fmaf(tz, 0.14f - 0.36f, 0.36f), fmaf(tz, 0.21f - 0.45f, 0.45f),
                        fmaf(tz, 0.49f - 0.57f, 0.57f));
             }
             break;
         }
-        const f3 pos = fmad3(d, h.dist, o);
+        const f3 pos = fmad3(d, best, o);
         f3 N;
-        if (h.sphere) {
-            N = fmad3(d, h.pt, o) - ld3f(p.sph[h.slot].cf);
+        if (slot < p.nS) {
+            const float* S = p.s32[slot >> 2].v[slot & 3];
+            N = fmad3(d, bpt, o) - F3(S[0], S[1], S[2]);
         } else {
-            N = ld3f(p.wal[h.slot].nf);
+            const Wall32& Wl = p.w32[slot - p.nS];
+            N = F3(Wl.n[0], Wl.n[1], Wl.n[2]);
         }
-        const DevMat& m = p.mat[h.j];
+        const DevMat& m = p.mat[slot];
         const float kd = (float)m.kd, ks = (float)m.ks, ka = (float)m.ka, ex = (float)m.ex;
-        const f3 nv = d * frsq(a);
         const f3 nn = fnormalize(N);
         const f3 ldir = fnormalize(-pos);
         const float lamb = fmaxf(fdot(ldir, nn), 0.0f);
         const float res = fmaxf(fdot(fnormalize(ldir - nv), nn), 0.0f);
-        float s = fmaf(lamb, kd, fmaf(fpow(res, ex), ks, ka));
+        const float s = fmaf(lamb, kd, fmaf(fpow(res, ex), ks, ka));
         float ksun = 0.0f;
         if (sun) {
             const f3 sd = fnormalize(F3(.7f, .4f, .7f));
@@ -471,7 +522,7 @@ __device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, int&
         }
         st_s[k] = s;
         st_k[k] = ksun;
-        st_j[k] = h.j;
+        st_m[k] = slot;
         n = k + 1;
         const float cc = 2.0f * fdot(nv, nn);
         o = fmad3(N, 1e-4f, pos);
@@ -479,7 +530,7 @@ __device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, int&
     }
     for (int q = MAXD - 1; q >= 0; --q) {
         if (q < n) {
-            const DevMat& m = p.mat[st_j[q]];
+            const DevMat& m = p.mat[st_m[q]];
             const f3 col = F3((float)m.color[0], (float)m.color[1], (float)m.color[2]);
             f3 L = col * st_s[q];
             if (sun) L = fmad3(F3(1.64f * col.x, 1.27f * col.y, 0.99f * col.z), st_k[q], L);
@@ -522,8 +573,7 @@ __device__ __forceinline__ void store_pixel(const KParams& p, int r, int x, doub
 
 __device__ __forceinline__ void count_segments(const KParams& p, int segs) {
     if (p.segs == nullptr) return;
-    // wave reduction (64 lanes), one atomic per wave
-    for (int off = 32; off > 0; off >>= 1) segs += __shfl_xor(segs, off, 64);
+    for (int off = 32; off > 0; off >>= 1) segs += __shfl_xor(segs, off, 64);  // wave64 sum
     if ((threadIdx.x & 63) == 0) atomicAdd(p.segs, (unsigned long long)segs);
 }
 
@@ -571,6 +621,56 @@ int launch_trace(const KParams& p, int prec, void* stream) {
         case PREC_MIXED: return (int)launch_prec<PREC_MIXED>(p, grid, st);
         default: return (int)hipErrorInvalidValue;
     }
+}
+
+/* ------------------------------------------------------------------------ */
+/* self-test of the exact helpers (rt_selftest)                              */
+/* ------------------------------------------------------------------------ */
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+/* random doubles spanning the magnitudes the kernel divides: 2^-40 .. 2^40, both signs */
+__device__ __forceinline__ double rnd_double(uint64_t bits) {
+    const uint64_t mant = bits & 0xFFFFFFFFFFFFFull;
+    const uint64_t ex = 1023 - 40 + ((bits >> 52) % 81);
+    const uint64_t sign = (bits >> 63) << 63;
+    return __longlong_as_double((long long)(sign | (ex << 52) | mant));
+}
+
+__global__ void k_selftest(int which, uint64_t n, uint64_t seed, unsigned long long* bad) {
+    unsigned long long nbad = 0;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t z0 = mix64(seed + 3 * i), z1 = mix64(seed + 3 * i + 1);
+        if (which == 0) {
+            const double a = rnd_double(z0), b = rnd_double(z1);
+            const double q = div_r(a, b, rcp_refined(b));
+            if (__double_as_longlong(q) != __double_as_longlong(a / b)) ++nbad;
+            // the normalisation pattern: component / sqrt(sum of squares)
+            const double c = rnd_double(mix64(seed + 3 * i + 2));
+            const double l = sqrt(a * a + b * b + c * c);
+            const double q2 = div_r(c, l, rcp_refined(l));
+            if (__double_as_longlong(q2) != __double_as_longlong(c / l)) ++nbad;
+        } else {
+            const double x = (double)(z0 >> 11) * (1.0 / 9007199254740992.0);  // [0,1)
+            const double e = (double)(1 + (z1 % 64));
+            const double ref = pow(x, e), got = pow_e(x, e);
+            // squaring compounds rounding: x^64 carries up to ~63u
+            const double tol = 128.0 * 2.220446049250313e-16 * fabs(ref) + 1e-300;
+            if (fabs(got - ref) > tol) ++nbad;
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) nbad += __shfl_xor(nbad, off, 64);
+    if ((threadIdx.x & 63) == 0 && nbad) atomicAdd(bad, nbad);
+}
+
+int launch_selftest(int which, uint64_t n, uint64_t seed, unsigned long long* d_bad,
+                    void* stream) {
+    hipLaunchKernelGGL(k_selftest, dim3(1024), dim3(256), 0, static_cast<hipStream_t>(stream),
+                       which, n, seed, d_bad);
+    return (int)hipGetLastError();
 }
 
 }  // namespace rt

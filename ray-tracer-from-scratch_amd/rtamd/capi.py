@@ -102,6 +102,8 @@ SIGNATURES = [
     ("rt_band_rows", C.c_int,
      [C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     ("rt_max_depth", C.c_int32, []),
+    ("rt_selftest", C.c_int, [C.c_void_p, C.c_int32, C.c_uint64, C.c_uint64,
+                              C.POINTER(C.c_uint64)]),
 ]
 
 _lib = None
@@ -208,6 +210,11 @@ class Renderer:
         arr = (rt_prim * len(prims))(*prims)
         self._prims = arr
         check(self.lib.rt_set_scene(self.ctx, arr, len(prims)), self.ctx)
+
+    def selftest(self, test: int, n: int, seed: int = 1) -> int:
+        bad = C.c_uint64()
+        check(self.lib.rt_selftest(self.ctx, test, n, seed, C.byref(bad)), self.ctx)
+        return bad.value
 
     def render(self, cam: rt_camera, depth: int, precision: int = RT_PREC_F64, flags: int = 0,
                out_format: int = RT_OUT_RGB_F32, row0: int = 0, nrows: int | None = None,

@@ -24,6 +24,13 @@ timeout -k 10 300 python bench.py ${BENCH_ARGS:-} > "$OUT/bench.json" 2> "$OUT/b
 rc=$?; echo "bench rc=$rc"; cat "$OUT/bench.json"; tail -5 "$OUT/bench.err"
 [ $rc -eq 0 ] || exit $rc
 
+if [ "${SWEEP:-1}" = 1 ]; then
+  step sweep
+  timeout -k 10 300 python tools/sweep.py > "$OUT/sweep.jsonl" 2> "$OUT/sweep.err"
+  rc=$?; echo "sweep rc=$rc"; cat "$OUT/sweep.jsonl"
+  [ $rc -eq 0 ] || exit $rc
+fi
+
 if [ "${PROFILE:-1}" = 1 ]; then
   step rocprof
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
