@@ -95,7 +95,9 @@ typedef struct rt_camera {
 enum rt_precision {
     RT_PREC_F64 = 0,     /* fp64 everywhere, op-for-op the reference's arithmetic (parity) */
     RT_PREC_F32 = 1,     /* fp32 everywhere (throughput; flips at discontinuities) */
-    RT_PREC_MIXED = 2    /* fp32 conservative cull + fp64 exact on survivors: output == F64 */
+    RT_PREC_MIXED = 2,   /* fp32 conservative cull + fp64 exact on survivors: output == F64 */
+    RT_PREC_PATH64 = 3   /* F64's exact ray paths (hits, normals, reflections) + fp32 colour
+                            arithmetic: no discontinuity flips, colours within ~1e-6 */
 };
 
 enum rt_out_format {
@@ -164,7 +166,8 @@ int32_t rt_max_depth(void);
 /* ---- diagnostics -------------------------------------------------------- */
 /* Device self-test of the fp64 helpers the exact path relies on, over n seeded random
  * operands: test 0 = division with a shared refined reciprocal vs IEEE `/` (bitwise),
- * test 1 = integer-exponent pow by squaring vs pow() (within 128 ulp).
+ * test 1 = integer-exponent pow by squaring vs pow() (within 128 ulp),
+ * test 2 = the range-restricted sqrt sequence vs sqrt() (bitwise).
  * *mismatches receives the number of failures (0 expected). */
 int rt_selftest(rt_ctx* ctx, int32_t test, uint64_t n, uint64_t seed, uint64_t* mismatches);
 

@@ -24,6 +24,7 @@ struct rt_ctx {
     size_t scene_bytes = 0;
     bool have_scene = false;
     int nS = 0, nW = 0, nP = 0;
+    bool int_exp = true;
     size_t off_s64 = 0, off_w32 = 0, off_w64 = 0, off_sj = 0, off_wj = 0, off_mat = 0;
     void* d_out = nullptr;
     size_t d_out_cap = 0;
@@ -77,7 +78,7 @@ int check_render_args(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, int
     if (row0 < 0 || row0 + nrows > cam->height) return RT_ERR_OUT_OF_RANGE;
     if (depth < 0) return RT_ERR_INVALID_ARG;
     if (depth > rt::max_depth()) return RT_ERR_UNSUPPORTED;
-    if (precision < RT_PREC_F64 || precision > RT_PREC_MIXED) return RT_ERR_INVALID_ARG;
+    if (precision < RT_PREC_F64 || precision > RT_PREC_PATH64) return RT_ERR_INVALID_ARG;
     if (bytes_per_pixel(out_format) == 0) return RT_ERR_INVALID_ARG;
     return RT_OK;
 }
@@ -96,6 +97,7 @@ rt::KParams make_params(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, i
     p.mat = reinterpret_cast<const rt::DevMat*>(base + ctx->off_mat);
     p.nS = ctx->nS;
     p.nW = ctx->nW;
+    p.int_exp = ctx->int_exp ? 1 : 0;
     p.W = cam->width;
     p.row0 = row0;
     p.nrows = nrows;
@@ -332,6 +334,11 @@ int rt_set_scene(rt_ctx* ctx, const rt_prim* prims, int32_t n) {
     ctx->nS = (int)nS;
     ctx->nW = (int)nW;
     ctx->nP = n;
+    ctx->int_exp = true;
+    for (size_t k = 0; k < nS + nW; k++) {
+        const double e = mat[k].ex;
+        if (!(e >= 0.0 && e <= 1024.0 && e == std::floor(e))) ctx->int_exp = false;
+    }
     ctx->off_s64 = off_s64;
     ctx->off_w32 = off_w32;
     ctx->off_w64 = off_w64;
@@ -343,7 +350,7 @@ int rt_set_scene(rt_ctx* ctx, const rt_prim* prims, int32_t n) {
 }
 
 int rt_selftest(rt_ctx* ctx, int32_t test, uint64_t n, uint64_t seed, uint64_t* mismatches) {
-    if (!ctx || !mismatches || test < 0 || test > 1) return RT_ERR_INVALID_ARG;
+    if (!ctx || !mismatches || test < 0 || test > 2) return RT_ERR_INVALID_ARG;
     RT_HIP(ctx, hipSetDevice(ctx->device));
     RT_HIP(ctx, hipMemsetAsync(ctx->d_segs, 0, sizeof(unsigned long long), ctx->stream));
     const int e = rt::launch_selftest(test, n, seed, ctx->d_segs, ctx->stream);

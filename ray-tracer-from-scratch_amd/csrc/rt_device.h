@@ -50,7 +50,7 @@ static_assert(sizeof(SphG32) == 64 && sizeof(SphG64) == 128, "sphere group layou
 static_assert(sizeof(Wall32) == 64 && sizeof(Wall64) == 128, "wall layout");
 static_assert(sizeof(DevMat) == 64, "material layout");
 
-enum { PREC_F64 = 0, PREC_F32 = 1, PREC_MIXED = 2 };
+enum { PREC_F64 = 0, PREC_F32 = 1, PREC_MIXED = 2, PREC_PATH64 = 3 };
 enum { OUT_RGB_F32 = 0, OUT_RGB_F64 = 1, OUT_RGBA8 = 2 };
 enum { FLAG_SUN = 1 };
 
@@ -68,6 +68,7 @@ struct KParams {
     const int32_t* wall_j;
     const DevMat* mat;     // [nS + nW]
     int32_t nS, nW;
+    int32_t int_exp;       // every specular exponent is an integer in [0, 1024]
     int32_t W, row0, nrows, depth;
     uint32_t flags;
     int32_t outf;
@@ -80,8 +81,9 @@ struct KParams {
 int launch_trace(const KParams& p, int prec, void* stream);
 int max_depth();
 // Device self-test of the exact fp64 helpers against IEEE operations:
-// which 0 = division (shared reciprocal), 1 = integer-exponent pow vs pow();
-// adds the number of mismatches (division: bitwise; pow: > 128 ulp) to *d_bad.
+// which 0 = division (shared reciprocal), 1 = integer-exponent pow vs pow(),
+// 2 = sqrt_e vs sqrt(); adds the number of mismatches (division, sqrt: bitwise;
+// pow: > 128 ulp) to *d_bad.
 int launch_selftest(int which, uint64_t n, uint64_t seed, unsigned long long* d_bad,
                     void* stream);
 

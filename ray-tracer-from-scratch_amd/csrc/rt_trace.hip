@@ -18,6 +18,9 @@
  *              throughput path; flips at geometric discontinuities.
  *   PREC_MIXED fp32 conservative cull in the primitive scan, PREC_F64's exact test on
  *              every primitive the cull cannot reject, fp64 shading: output == F64.
+ *   PREC_PATH64 PREC_F64's exact ray path (hits, positions, normals, reflections) with
+ *              the colour arithmetic (shading, sky, lerp) in fp32: every pixel follows the
+ *              reference's path, colours within ~1e-6 (no discontinuity flips).
  *
  * Exact rewrites (each identity holds in IEEE binary64 barring overflow/underflow):
  *   - b = 2*dot(d,oc) is exact, so b*b - (4a)*c == 4*(dot*dot - a*c) and
@@ -39,6 +42,8 @@
 
 #include <float.h>
 #include <math.h>
+
+#include <type_traits>
 
 #include "rt_device.h"
 
@@ -78,28 +83,49 @@ __device__ __forceinline__ double div_r(double a, double b, double r) {
     const double q1 = __builtin_fma(e, r, q);
     return a == 0.0 ? q : q1;
 }
+/* sqrt(x) correctly rounded: LLVM's fp64 sqrt sequence (rsq + Goldschmidt/Newton
+ * refinement) without its range scaling, which is the identity for x >= 2^-767; smaller
+ * (and zero/negative) arguments take the library path. */
+__device__ __forceinline__ double sqrt_e(double x) {
+    if (!(x >= 0x1p-767)) return sqrt(x);
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y;
+    double h = y * 0.5;
+    const double r = __builtin_fma(-h, g, 0.5);
+    g = __builtin_fma(g, r, g);
+    double d = __builtin_fma(-g, g, x);
+    h = __builtin_fma(h, r, h);
+    g = __builtin_fma(d, h, g);
+    d = __builtin_fma(-g, g, x);
+    return __builtin_fma(d, h, g);
+}
 /* v / len(v) component-wise (vec.cpp:21), one shared reciprocal. */
 __device__ __forceinline__ d3 normalize_e(d3 v) {
-    const double l = sqrt(lensq(v));
+    const double l = sqrt_e(lensq(v));
     const double r = rcp_refined(l);
     return D3(div_r(v.x, l, r), div_r(v.y, l, r), div_r(v.z, l, r));
 }
 __device__ __forceinline__ d3 div3(d3 v, double l, double r) {
     return D3(div_r(v.x, l, r), div_r(v.y, l, r), div_r(v.z, l, r));
 }
-/* x^e for x >= 0: binary powering when e is a small non-negative integer (every
- * material in the reference and the configs: 30, 50), else pow(). */
-__device__ __forceinline__ double pow_e(double x, double e) {
-    if (e >= 0.0 && e <= 1024.0 && e == __builtin_rint(e)) {
-        int n = (int)e;
-        double acc = 1.0, b = x;
-        while (n) {
-            if (n & 1) acc *= b;
-            n >>= 1;
-            if (n) b *= b;
-        }
-        return acc;
+/* x^n for x >= 0 and integer n >= 0 by binary powering. */
+__device__ __forceinline__ double pow_int(double x, int n) {
+    double acc = 1.0, b = x;
+    while (n) {
+        if (n & 1) acc *= b;
+        n >>= 1;
+        if (n) b *= b;
     }
+    return acc;
+}
+/* x^e for x >= 0.  INT_EXP (host-checked at rt_set_scene: every specular exponent is an
+ * integer in [0, 1024], as in the reference scene and all configs: 30, 50) compiles only
+ * the binary powering; otherwise the general pow() is kept — it is large, and its
+ * register footprint counts for the whole kernel even where it never runs. */
+template <bool INT_EXP>
+__device__ __forceinline__ double pow_e(double x, double e) {
+    if (INT_EXP) return pow_int(x, (int)e);
+    if (e >= 0.0 && e <= 1024.0 && e == __builtin_rint(e)) return pow_int(x, (int)e);
     return pow(x, e);
 }
 
@@ -179,7 +205,7 @@ __device__ __forceinline__ void sphere_exact(const double* S, int s, const RayD&
         pt = div_r(-dt, r.a, r.ra);  // -b / (2a)
         proj = 2.0 * pt;             // (-b - sqrt(0)) / a: scene.cpp:65's /a kept
     } else {
-        const double num = -dt - sqrt(x);
+        const double num = -dt - sqrt_e(x);
         if (!(num > 0)) return;
         proj = div_r(num, r.a, r.ra);
         pt = proj;
@@ -308,7 +334,7 @@ __device__ __forceinline__ HitD closest_hit_d(const KParams& p, const RayD& r) {
 /* out_color, main.cpp:28-37: only normalize(v).z is used; z^0.25 as sqrt(sqrt(z)). */
 __device__ __forceinline__ d3 sky_d(const RayD& r, double nvz) {
     if (r.d.z < 0.0) return ground_color();
-    return lerp(sky_low(), sky_high(), sqrt(sqrt(nvz)));
+    return lerp(sky_low(), sky_high(), sqrt_e(sqrt_e(nvz)));
 }
 
 /* Shading of one hit (main.cpp:99-104 + diffuse_shading + specular), returning
@@ -319,6 +345,7 @@ struct ShadeD {
     double s;
     double ksun;
 };
+template <bool INT_EXP>
 __device__ __forceinline__ ShadeD shade_d(const DevMat& m, const d3 pos, const d3 nn,
                                           const d3 view, bool sun) {
     const d3 ldir = normalize_e(D3(0.0 - pos.x, 0.0 - pos.y, 0.0 - pos.z));  // LIGHT_POS - pos
@@ -326,7 +353,7 @@ __device__ __forceinline__ ShadeD shade_d(const DevMat& m, const d3 pos, const d
     const double diffuse = lamb > 0 ? lamb : 0;
     double res = dot(normalize_e(view + ldir), nn);
     res = res > 0 ? res : 0;
-    const double spec = pow_e(res, m.ex);
+    const double spec = pow_e<INT_EXP>(res, m.ex);
     ShadeD sh;
     sh.s = diffuse * m.kd + spec * m.ks + m.ka;
     sh.ksun = 0;
@@ -336,7 +363,7 @@ __device__ __forceinline__ ShadeD shade_d(const DevMat& m, const d3 pos, const d
         a = a > 0 ? a : 0;
         double hs = dot(normalize_e(view + sd), nn);
         hs = hs > 0 ? hs : 0;
-        sh.ksun = a * m.kd + pow_e(hs, m.ex) * m.ks;
+        sh.ksun = a * m.kd + pow_e<INT_EXP>(hs, m.ex) * m.ks;
     }
     return sh;
 }
@@ -356,29 +383,68 @@ __device__ __forceinline__ RayD make_ray(d3 o, d3 d) {
     r.d = d;
     r.a = lensq(d);
     r.ra = rcp_refined(r.a);
-    r.dlen = sqrt(r.a);
+    r.dlen = sqrt_e(r.a);
     return r;
 }
 
-template <bool MIXED, int MAXD>
+/* fp32 shading of one hit for PATH64: the same formulas as shade_d on the exact fp64
+ * geometry rounded to fp32 (colour only — nothing here feeds the next ray). */
+__device__ __forceinline__ float2 shade_f(const DevMat& m, const f3 pos, const f3 nn,
+                                          const f3 nv, bool sun) {
+    const float kd = (float)m.kd, ks = (float)m.ks, ka = (float)m.ka, ex = (float)m.ex;
+    const f3 ldir = fnormalize(-pos);
+    const float lamb = fmaxf(fdot(ldir, nn), 0.0f);
+    const float res = fmaxf(fdot(fnormalize(ldir - nv), nn), 0.0f);
+    float2 r;
+    r.x = fmaf(lamb, kd, fmaf(fpow(res, ex), ks, ka));
+    r.y = 0.0f;
+    if (sun) {
+        const f3 sd = fnormalize(F3(.7f, .4f, .7f));
+        const float sa = fmaxf(fdot(sd, nn), 0.0f);
+        const float hs = fmaxf(fdot(fnormalize(sd - nv), nn), 0.0f);
+        r.y = fmaf(sa, kd, fpow(hs, ex) * ks);
+    }
+    return r;
+}
+__device__ __forceinline__ f3 local_color_f(const DevMat& m, float s, float ksun, bool sun) {
+    const f3 col = F3((float)m.color[0], (float)m.color[1], (float)m.color[2]);
+    f3 L = col * s;
+    if (sun) L = fmad3(F3(1.64f * col.x, 1.27f * col.y, 0.99f * col.z), ksun, L);
+    return L;
+}
+__device__ __forceinline__ f3 tof(d3 v) { return F3((float)v.x, (float)v.y, (float)v.z); }
+
+/* One pixel on the exact fp64 ray path.  COLOR64: colour arithmetic in fp64 too (F64 /
+ * MIXED, the parity modes); otherwise in fp32 (PATH64). */
+template <bool MIXED, bool COLOR64, bool SUN, bool INT_EXP, int MAXD>
 __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, int& segs) {
+    using CT = typename std::conditional<COLOR64, double, float>::type;
     const d3 cpos = ld3(p.pos);
     const d3 pc = (ld3(p.tl) + ld3(p.dx) * (double)x) + ld3(p.dy) * (double)i;  // main.cpp:132
     RayD r = make_ray(cpos, cpos - pc);  // main.cpp:133-134 (direction not normalised)
-    const bool sun = (p.flags & FLAG_SUN) != 0;
+    constexpr bool sun = SUN;
 
-    double st_s[MAXD];
-    double st_k[MAXD];
+    CT st_s[MAXD];
+    CT st_k[MAXD];
     int st_m[MAXD];
     int n = 0;
-    d3 c;
+    d3 c64;
+    f3 c32;
     for (int k = 0;; ++k) {
         ++segs;
         const HitD h = closest_hit_d<MIXED>(p, r);
         const double rdl = rcp_refined(r.dlen);
         const d3 nv = div3(r.d, r.dlen, rdl);  // normalize(d); normalize(-d) == -nv
         if (h.slot < 0) {
-            c = sky_d(r, nv.z);
+            if (COLOR64) {
+                c64 = sky_d(r, nv.z);
+            } else if (r.d.z < 0.0) {
+                c32 = F3(0.025f, 0.05f, 0.075f);
+            } else {
+                const float tz = fsqrt(fsqrt((float)nv.z));
+                c32 = F3(fmaf(tz, 0.14f - 0.36f, 0.36f), fmaf(tz, 0.21f - 0.45f, 0.45f),
+                         fmaf(tz, 0.49f - 0.57f, 0.57f));
+            }
             break;
         }
         const d3 pos = r.o + r.d * h.dist;  // main.cpp:99 (sphere world distance used as t)
@@ -391,13 +457,25 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, int&
         }
         const DevMat& m = p.mat[h.slot];
         const d3 nn = normalize_e(N);
-        const ShadeD sh = shade_d(m, pos, nn, -nv, sun);
+        CT s, ks;
+        if (COLOR64) {
+            const ShadeD sh = shade_d<INT_EXP>(m, pos, nn, -nv, sun);
+            s = sh.s;
+            ks = sh.ksun;
+        } else {
+            const float2 sh = shade_f(m, tof(pos), tof(nn), tof(nv), sun);
+            s = sh.x;
+            ks = sh.y;
+        }
         if (k >= p.depth || k >= MAXD) {  // remaining_iterations <= 0 (main.cpp:105)
-            c = local_color_d(m, sh.s, sh.ksun, sun);
+            if (COLOR64)
+                c64 = local_color_d(m, s, ks, sun);
+            else
+                c32 = local_color_f(m, s, ks, sun);
             break;
         }
-        st_s[k] = sh.s;
-        st_k[k] = sh.ksun;
+        st_s[k] = s;
+        st_k[k] = ks;
         st_m[k] = h.slot;
         n = k + 1;
         // start + reflect(d, N) (main.cpp:111-113, vec.cpp:51-57)
@@ -407,23 +485,31 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, int&
     for (int q = MAXD - 1; q >= 0; --q) {
         if (q < n) {
             const DevMat& m = p.mat[st_m[q]];
-            const d3 L = local_color_d(m, st_s[q], st_k[q], sun);
-            c = lerp(L, c, m.km);  // vec.cpp:45-49 via main.cpp:117
+            if (COLOR64) {
+                const d3 L = local_color_d(m, st_s[q], st_k[q], sun);
+                c64 = lerp(L, c64, m.km);  // vec.cpp:45-49 via main.cpp:117
+            } else {
+                const f3 L = local_color_f(m, st_s[q], st_k[q], sun);
+                const float km = (float)m.km;
+                c32 = F3(fmaf(km, c32.x - L.x, L.x), fmaf(km, c32.y - L.y, L.y),
+                         fmaf(km, c32.z - L.z, L.z));
+            }
         }
     }
-    return c;
+    if (COLOR64) return c64;
+    return D3(c32.x, c32.y, c32.z);
 }
 
 /* ------------------------------------------------------------------------ */
 /* fp32 throughput path                                                      */
 /* ------------------------------------------------------------------------ */
-template <int MAXD>
+template <bool SUN, int MAXD>
 __device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, int& segs) {
     const d3 pcd = (ld3(p.tl) + ld3(p.dx) * (double)x) + ld3(p.dy) * (double)i;
     const d3 dd = ld3(p.pos) - pcd;
     f3 o = F3((float)p.pos[0], (float)p.pos[1], (float)p.pos[2]);
     f3 d = F3((float)dd.x, (float)dd.y, (float)dd.z);
-    const bool sun = (p.flags & FLAG_SUN) != 0;
+    constexpr bool sun = SUN;
 
     float st_s[MAXD];
     float st_k[MAXD];
@@ -577,8 +663,20 @@ __device__ __forceinline__ void count_segments(const KParams& p, int segs) {
     if ((threadIdx.x & 63) == 0) atomicAdd(p.segs, (unsigned long long)segs);
 }
 
-template <int PREC, int MAXD>
-__global__ void __launch_bounds__(BLOCK) k_trace(KParams p) {
+/* Occupancy target per instantiation (waves per SIMD; MI355X_MICROARCH.md: <= 128 VGPRs
+ * for 4, <= 96 for 5).  The fp64-colour paths carry the most state. */
+template <int PREC, bool SUN, bool INT_EXP, int MAXD>
+constexpr int waves_per_eu() {
+    if (PREC == PREC_F32) return 5;
+    if (PREC == PREC_PATH64) return 4;
+    const int w = INT_EXP ? (SUN ? 3 : 4) : (SUN ? 2 : 3);
+    return (MAXD >= 16 && w > 2) ? w - 1 : w;
+}
+
+template <int PREC, bool SUN, bool INT_EXP, int MAXD>
+__global__ void __launch_bounds__(BLOCK)
+__attribute__((amdgpu_waves_per_eu(waves_per_eu<PREC, SUN, INT_EXP, MAXD>(), 8)))
+k_trace(KParams p) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int x = blockIdx.x * TILE_W + (wave & 1) * 8 + (lane & 7);
@@ -588,25 +686,41 @@ __global__ void __launch_bounds__(BLOCK) k_trace(KParams p) {
     if (valid) {
         const int i = p.row0 + r;
         if (PREC == PREC_F32) {
-            const f3 c = trace_pixel_f<MAXD>(p, x, i, segs);
+            const f3 c = trace_pixel_f<SUN, MAXD>(p, x, i, segs);
             store_pixel(p, r, x, c.x, c.y, c.z);
         } else {
-            const d3 c = trace_pixel_d<PREC == PREC_MIXED, MAXD>(p, x, i, segs);
+            const d3 c =
+                trace_pixel_d<PREC == PREC_MIXED, PREC != PREC_PATH64, SUN, INT_EXP, MAXD>(
+                    p, x, i, segs);
             store_pixel(p, r, x, c.x, c.y, c.z);
         }
     }
     count_segments(p, segs);
 }
 
-template <int PREC>
+template <int PREC, bool SUN, bool INT_EXP>
 static hipError_t launch_prec(const KParams& p, dim3 grid, hipStream_t st) {
     if (p.depth <= MAXD_SMALL)
-        hipLaunchKernelGGL((k_trace<PREC, MAXD_SMALL>), grid, dim3(BLOCK), 0, st, p);
+        hipLaunchKernelGGL((k_trace<PREC, SUN, INT_EXP, MAXD_SMALL>), grid, dim3(BLOCK), 0, st, p);
     else if (p.depth <= MAXD_MID)
-        hipLaunchKernelGGL((k_trace<PREC, MAXD_MID>), grid, dim3(BLOCK), 0, st, p);
+        hipLaunchKernelGGL((k_trace<PREC, SUN, INT_EXP, MAXD_MID>), grid, dim3(BLOCK), 0, st, p);
     else
-        hipLaunchKernelGGL((k_trace<PREC, MAXD_LARGE>), grid, dim3(BLOCK), 0, st, p);
+        hipLaunchKernelGGL((k_trace<PREC, SUN, INT_EXP, MAXD_LARGE>), grid, dim3(BLOCK), 0, st, p);
     return hipGetLastError();
+}
+template <int PREC>
+static hipError_t launch_prec(const KParams& p, dim3 grid, hipStream_t st) {
+    // the fp32 colour paths never use the fp64 pow: one variant
+    if constexpr (PREC == PREC_F64 || PREC == PREC_MIXED) {
+        if (p.flags & FLAG_SUN)
+            return p.int_exp ? launch_prec<PREC, true, true>(p, grid, st)
+                             : launch_prec<PREC, true, false>(p, grid, st);
+        return p.int_exp ? launch_prec<PREC, false, true>(p, grid, st)
+                         : launch_prec<PREC, false, false>(p, grid, st);
+    } else {
+        return (p.flags & FLAG_SUN) ? launch_prec<PREC, true, true>(p, grid, st)
+                                    : launch_prec<PREC, false, true>(p, grid, st);
+    }
 }
 
 int max_depth() { return MAXD_LARGE; }
@@ -619,6 +733,7 @@ int launch_trace(const KParams& p, int prec, void* stream) {
         case PREC_F64: return (int)launch_prec<PREC_F64>(p, grid, st);
         case PREC_F32: return (int)launch_prec<PREC_F32>(p, grid, st);
         case PREC_MIXED: return (int)launch_prec<PREC_MIXED>(p, grid, st);
+        case PREC_PATH64: return (int)launch_prec<PREC_PATH64>(p, grid, st);
         default: return (int)hipErrorInvalidValue;
     }
 }
@@ -653,10 +768,15 @@ __global__ void k_selftest(int which, uint64_t n, uint64_t seed, unsigned long l
             const double l = sqrt(a * a + b * b + c * c);
             const double q2 = div_r(c, l, rcp_refined(l));
             if (__double_as_longlong(q2) != __double_as_longlong(c / l)) ++nbad;
+        } else if (which == 2) {
+            const double a = fabs(rnd_double(z0));
+            if (__double_as_longlong(sqrt_e(a)) != __double_as_longlong(sqrt(a))) ++nbad;
+            const double b = (double)(z1 >> 11) * (1.0 / 9007199254740992.0);  // [0,1)
+            if (__double_as_longlong(sqrt_e(b)) != __double_as_longlong(sqrt(b))) ++nbad;
         } else {
             const double x = (double)(z0 >> 11) * (1.0 / 9007199254740992.0);  // [0,1)
             const double e = (double)(1 + (z1 % 64));
-            const double ref = pow(x, e), got = pow_e(x, e);
+            const double ref = pow(x, e), got = pow_int(x, (int)e);
             // squaring compounds rounding: x^64 carries up to ~63u
             const double tol = 128.0 * 2.220446049250313e-16 * fabs(ref) + 1e-300;
             if (fabs(got - ref) > tol) ++nbad;

@@ -33,7 +33,9 @@ RT_PRIM_WALL = 1
 RT_PREC_F64 = 0
 RT_PREC_F32 = 1
 RT_PREC_MIXED = 2
-PRECISIONS = {"f64": RT_PREC_F64, "f32": RT_PREC_F32, "mixed": RT_PREC_MIXED}
+RT_PREC_PATH64 = 3
+PRECISIONS = {"f64": RT_PREC_F64, "f32": RT_PREC_F32, "mixed": RT_PREC_MIXED,
+              "path64": RT_PREC_PATH64}
 
 RT_OUT_RGB_F32 = 0
 RT_OUT_RGB_F64 = 1
