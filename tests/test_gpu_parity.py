@@ -286,3 +286,51 @@ def test_selftest_shared_reciprocal_division_is_ieee(rend):
 
 def test_selftest_integer_pow(rend):
     assert rend.selftest(1, 1 << 22, seed=777) == 0
+
+
+def test_selftest_sqrt_sequence_is_ieee(rend):
+    assert rend.selftest(2, 1 << 24, seed=4242) == 0
+
+
+# ---------------------------------------------------------------- PATH64
+PATH64_TOL = 2e-5   # fp32 colour arithmetic on the exact fp64 path (north_star bound: 1e-4)
+
+
+def test_path64_every_pixel_within_tolerance(rend, golden_frames):
+    """Exact fp64 ray paths + fp32 colour: no discontinuity flips, so EVERY pixel of every
+    golden frame (depth up to 10, 256 spheres) is within PATH64_TOL of the reference."""
+    for key in golden_frames.files:
+        name, w, h, depth = parse_frame_key(key)
+        img, _, _ = render(rend, scene_by_name(name), w, h, depth, capi.RT_PREC_PATH64)
+        d = np.abs(img - golden_frames[key]).max()
+        assert d <= PATH64_TOL, (key, d)
+
+
+@pytest.mark.parametrize("cfg_name", ["c2", "c3"])
+def test_path64_full_size_vs_f64(rend, cfg_name):
+    cfg = scenes.CONFIGS[cfg_name]
+    sc = cfg.scene()
+    a, sa, _ = render(rend, sc, cfg.width, cfg.height, cfg.depth, capi.RT_PREC_F64,
+                      count_segments=True)
+    b, sb, _ = render(rend, sc, cfg.width, cfg.height, cfg.depth, capi.RT_PREC_PATH64,
+                      count_segments=True)
+    assert sa.segments == sb.segments
+    assert np.abs(a - b).max() <= PATH64_TOL
+
+
+def test_path64_sun(rend, oracle):
+    sc = scenes.synthetic_scene(8, 4)
+    img, _, cam = render(rend, sc, 96, 54, 4, capi.RT_PREC_PATH64, flags=capi.RT_FLAG_SUN)
+    o64, _, _ = oracle.render(scenes.to_prims(sc), cam, 4, flags=capi.RT_FLAG_SUN)
+    assert np.abs(img - o64).max() <= 4 * PATH64_TOL   # sun adds up to 1.64x colour
+
+
+def test_non_integer_specular_exponent(rend, oracle):
+    """A material with a non-integer exponent selects the general-pow kernel variant."""
+    sc = scenes.synthetic_scene(6, 3, seed=3)
+    sc[0].mat.specular_exponent = 37.5
+    sc[2].mat.specular_exponent = 0.0
+    for prec in (capi.RT_PREC_F64, capi.RT_PREC_MIXED):
+        img, _, cam = render(rend, sc, 64, 36, 5, prec)
+        o64, _, _, sig = oracle.render(scenes.to_prims(sc), cam, 5, want_sig=True)
+        check_f64(img, o64, sig, what=("nonint", prec))

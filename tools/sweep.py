@@ -17,7 +17,7 @@ from rtamd import capi, scenes  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="c1,c2,c3,c5")
-    ap.add_argument("--precisions", default="f64,mixed,f32")
+    ap.add_argument("--precisions", default="f64,mixed,path64,f32")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--sun", action="store_true")
