@@ -130,6 +130,17 @@ int rt_capi_version(void);
  * device.  Replaces any previous scene.  n == 0 is a valid (empty) scene. */
 int rt_set_scene(rt_ctx* ctx, const rt_prim* prims, int32_t n);
 
+/* ---- tuning ------------------------------------------------------------- */
+enum rt_option {
+    RT_OPT_WAVE_CULL_MIN_SPHERES = 1, /* scenes with at least this many spheres use the
+                                         wave-cooperative cull (default 24; 0 = always,
+                                         INT32_MAX = never).  Output is identical. */
+    RT_OPT_STATS_DEVICE_PTR = 2       /* diagnostics: device address of 3 uint64 counters
+                                         that renders add to ([0] wave culls, [1] spheres
+                                         kept, [2] spheres considered); 0 = off */
+};
+int rt_set_option(rt_ctx* ctx, int32_t option, int64_t value);
+
 /* ---- frame operators (replace rt_scene, main.cpp:124-139) --------------- */
 /* Render rows [row0, row0+nrows) of the frame into caller-owned HOST memory `out`
  * (nrows*width pixels of `out_format`), synchronously.  depth = remaining_iterations

@@ -25,6 +25,8 @@ struct rt_ctx {
     bool have_scene = false;
     int nS = 0, nW = 0, nP = 0;
     bool int_exp = true;
+    unsigned long long* d_stats = nullptr;
+    int wave_cull_min = 24;  // spheres from which the wave cull pays (tools/sweep.py)
     size_t off_s64 = 0, off_w32 = 0, off_w64 = 0, off_sj = 0, off_wj = 0, off_mat = 0;
     void* d_out = nullptr;
     size_t d_out_cap = 0;
@@ -98,6 +100,7 @@ rt::KParams make_params(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, i
     p.nS = ctx->nS;
     p.nW = ctx->nW;
     p.int_exp = ctx->int_exp ? 1 : 0;
+    p.wave_cull = ctx->nS >= ctx->wave_cull_min ? 1 : 0;
     p.W = cam->width;
     p.row0 = row0;
     p.nrows = nrows;
@@ -112,6 +115,7 @@ rt::KParams make_params(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, i
     }
     p.out = d_out;
     p.segs = d_segs;
+    p.stats = ctx->d_stats;
     return p;
 }
 
@@ -347,6 +351,21 @@ int rt_set_scene(rt_ctx* ctx, const rt_prim* prims, int32_t n) {
     ctx->off_mat = off_mat;
     ctx->have_scene = true;
     return RT_OK;
+}
+
+int rt_set_option(rt_ctx* ctx, int32_t option, int64_t value) {
+    if (!ctx) return RT_ERR_INVALID_ARG;
+    switch (option) {
+        case RT_OPT_WAVE_CULL_MIN_SPHERES:
+            if (value < 0) return RT_ERR_INVALID_ARG;
+            ctx->wave_cull_min = value > 0x7fffffff ? 0x7fffffff : (int)value;
+            return RT_OK;
+        case RT_OPT_STATS_DEVICE_PTR:
+            ctx->d_stats = reinterpret_cast<unsigned long long*>(static_cast<intptr_t>(value));
+            return RT_OK;
+        default:
+            return RT_ERR_INVALID_ARG;
+    }
 }
 
 int rt_selftest(rt_ctx* ctx, int32_t test, uint64_t n, uint64_t seed, uint64_t* mismatches) {

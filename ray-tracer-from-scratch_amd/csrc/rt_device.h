@@ -69,12 +69,14 @@ struct KParams {
     const DevMat* mat;     // [nS + nW]
     int32_t nS, nW;
     int32_t int_exp;       // every specular exponent is an integer in [0, 1024]
+    int32_t wave_cull;     // cull spheres per wave (rt_trace.hip) before the per-lane tests
     int32_t W, row0, nrows, depth;
     uint32_t flags;
     int32_t outf;
     double pos[3], tl[3], dx[3], dy[3];
     void* out;
-    unsigned long long* segs;  // may be null
+    unsigned long long* segs;   // may be null
+    unsigned long long* stats;  // diagnostic counters, may be null (rt_set_option)
 };
 
 // Host-side launchers (rt_trace.hip).  Return a hipError_t as int.

@@ -193,7 +193,15 @@ struct RayD {
  *   x < 0 (det < 0)    -> miss (scene.cpp:57)
  *   -dot - sqrt(x) <= 0 -> proj <= 0, rejected
  * and p1 is never the minimum: (-b+sq)/2a >= (-b-sq)/2a by monotonic rounding. */
-__device__ __forceinline__ void sphere_exact(const double* S, int s, const RayD& r, HitD& h) {
+__device__ __forceinline__ int scene_index(const KParams& p, int slot) {
+    return slot < p.nS ? p.sph_j[slot] : p.wall_j[slot - p.nS];
+}
+
+/* IN_ORDER: spheres visited in increasing index before any wall, so a tie keeps the
+ * earlier hit (strict <, main.cpp:77); otherwise a tie compares scene indices. */
+template <bool IN_ORDER = true>
+__device__ __forceinline__ void sphere_exact(const double* S, int s, const RayD& r, HitD& h,
+                                             const KParams* p = nullptr) {
     const d3 oc = r.o - D3(S[0], S[1], S[2]);
     const double dt = dot(r.d, oc);  // b / 2
     if (dt > 0) return;
@@ -211,15 +219,14 @@ __device__ __forceinline__ void sphere_exact(const double* S, int s, const RayD&
         pt = proj;
     }
     const double dist = proj * r.dlen;  // world distance, scene.cpp:77
-    if (dist > 0 && dist < h.dist) {
+    bool take = dist > 0 && dist < h.dist;
+    if (!IN_ORDER && !take && dist > 0 && dist == h.dist && h.slot >= 0)
+        take = scene_index(*p, s) < scene_index(*p, h.slot);
+    if (take) {
         h.dist = dist;
         h.pt = pt;
         h.slot = s;
     }
-}
-
-__device__ __forceinline__ int scene_index(const KParams& p, int slot) {
-    return slot < p.nS ? p.sph_j[slot] : p.wall_j[slot - p.nS];
 }
 
 /* Wall::intersect (scene.cpp:4-35), exact.  t = num/denom is formed only when the signs
@@ -291,21 +298,255 @@ __device__ __forceinline__ bool wall_cull(const Wall32& Wl, const RayF& r) {
     return px < -err || px > Wl.len + err || py < -err || py > Wl.wid + err;
 }
 
-template <bool MIXED>
-__device__ __forceinline__ HitD closest_hit_d(const KParams& p, const RayD& r) {
+/* ------------------------------------------------------------------------ */
+/* wave-cooperative sphere cull                                              */
+/* ------------------------------------------------------------------------ */
+/* Every lane of a wave scans the same primitive list, so the wave can cull the list
+ * once for all its live rays: bound them by a cone (apex = centre of the origins' box,
+ * widened by its half-diagonal rho; axis = mean direction; half-angle = the widest
+ * direction), test 64 spheres at a time against it — lane l tests sphere c0 + l — and
+ * ballot the survivors.  A ray o_i + t d_i (t >= 0) that meets ball(C, r) puts
+ * o_c + t d_i inside ball(C, r + rho), so a sphere whose inflated ball misses the cone
+ * is missed by every live ray: the exact per-lane test would reject it (det < 0 or no
+ * positive root).  Margins (1e-4 relative + absolute) dwarf the fp32 error of the bound.
+ * Cost per bounce: ten wave reductions + ceil(nS/64) cull passes; enabled by the host
+ * when the scene is large enough to pay for it (KParams::wave_cull). */
+/* Wave64 reductions returning a wave-uniform (scalar) value: a butterfly inside each
+ * 16-lane row with DPP (xor 1, xor 2, half-mirror, mirror — each step leaves groups
+ * uniform, so a mirror acts as the next xor), then the four row results read out with
+ * v_readlane.  Every lane must be active (the bounce loops are converged). */
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float lane_f(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ float wsum(float v) {
+    v += dpp<0xB1>(v);
+    v += dpp<0x4E>(v);
+    v += dpp<0x141>(v);
+    v += dpp<0x140>(v);
+    return (lane_f(v, 0) + lane_f(v, 16)) + (lane_f(v, 32) + lane_f(v, 48));
+}
+__device__ __forceinline__ float wmin(float v) {
+    v = fminf(v, dpp<0xB1>(v));
+    v = fminf(v, dpp<0x4E>(v));
+    v = fminf(v, dpp<0x141>(v));
+    v = fminf(v, dpp<0x140>(v));
+    return fminf(fminf(lane_f(v, 0), lane_f(v, 16)), fminf(lane_f(v, 32), lane_f(v, 48)));
+}
+__device__ __forceinline__ float wmax(float v) {
+    v = fmaxf(v, dpp<0xB1>(v));
+    v = fmaxf(v, dpp<0x4E>(v));
+    v = fmaxf(v, dpp<0x141>(v));
+    v = fmaxf(v, dpp<0x140>(v));
+    return fmaxf(fmaxf(lane_f(v, 0), lane_f(v, 16)), fmaxf(lane_f(v, 32), lane_f(v, 48)));
+}
+__device__ __forceinline__ float uni(float v) { return v; }  // reductions are already scalar
+
+struct Cone {
+    f3 apex;
+    f3 u;
+    float rho, cos_t, sin_t, scale;
+    bool on;
+};
+
+__device__ __forceinline__ Cone wave_cone(f3 o, f3 d, bool alive) {
+    Cone c;
+    const float inf = __builtin_inff();
+    const f3 lo = F3(uni(wmin(alive ? o.x : inf)), uni(wmin(alive ? o.y : inf)),
+                     uni(wmin(alive ? o.z : inf)));
+    const f3 hi = F3(uni(wmax(alive ? o.x : -inf)), uni(wmax(alive ? o.y : -inf)),
+                     uni(wmax(alive ? o.z : -inf)));
+    c.apex = (lo + hi) * 0.5f;
+    const f3 ext = (hi - lo) * 0.5f;
+    c.rho = fsqrt(fdot(ext, ext)) * 1.0001f;
+    c.scale = fmax3abs(c.apex.x, c.apex.y, c.apex.z) + c.rho;
+    const f3 dn = alive ? fnormalize(d) : F3(0.f, 0.f, 0.f);
+    const f3 su = F3(uni(wsum(dn.x)), uni(wsum(dn.y)), uni(wsum(dn.z)));
+    c.u = fnormalize(su);
+    c.cos_t = uni(wmin(alive ? fdot(c.u, dn) : 1.0f)) - 1e-4f;
+    c.sin_t = fsqrt(fmaxf(0.0f, 1.0f - c.cos_t * c.cos_t));
+    c.on = c.cos_t > 0.05f;  // a near-hemispherical fan culls nothing: skip the pass
+    return c;
+}
+
+/* Ballot of the spheres in [c0, c0+64) that may be hit by a live ray of the wave. */
+__device__ __forceinline__ uint64_t cull_chunk_raw(const KParams& p, const Cone& cn, int c0) {
+    const int s = c0 + (int)(threadIdx.x & 63);
+    bool keep = false;
+    if (s < p.nS) {
+        keep = true;
+        if (cn.on) {
+            const float* S = p.s32[s >> 2].v[s & 3];
+            const f3 v = F3(S[0], S[1], S[2]) - cn.apex;
+            const float L2 = fdot(v, v);
+            const float R = S[3] + cn.rho +
+                            1e-4f * (1.0f + cn.scale + fmax3abs(S[0], S[1], S[2]) + S[3]);
+            if (L2 > R * R) {  // apex outside the inflated ball
+                const float il = frsq(L2);
+                const float sa = fminf(R * il, 1.0f);
+                const float ca = fsqrt(fmaxf(0.0f, 1.0f - sa * sa));
+                const float cphi = fdot(cn.u, v) * il;
+                keep = cphi >= cn.cos_t * ca - cn.sin_t * sa - 1e-4f;
+            }
+        }
+    }
+    return __ballot(keep);
+}
+/* ... plus the optional diagnostic counters (KParams::stats: [0] culls, [1] spheres kept,
+ * [2] spheres considered) — one lane, one atomic each, only when stats are requested. */
+__device__ __forceinline__ uint64_t cull_chunk(const KParams& p, const Cone& cn, int c0) {
+    const uint64_t m = cull_chunk_raw(p, cn, c0);
+    if (p.stats != nullptr && (threadIdx.x & 63) == 0) {
+        const int nin = p.nS - c0 < 64 ? p.nS - c0 : 64;
+        atomicAdd(p.stats + 0, 1ull);
+        atomicAdd(p.stats + 1, (unsigned long long)__popcll(m));
+        atomicAdd(p.stats + 2, (unsigned long long)nin);
+    }
+    return m;
+}
+
+__device__ __forceinline__ RayF make_rayf(const RayD& r) {
+    RayF rf;
+    rf.o = F3((float)r.o.x, (float)r.o.y, (float)r.o.z);
+    rf.d = F3((float)r.d.x, (float)r.d.y, (float)r.d.z);
+    rf.a = fdot(rf.d, rf.d);
+    rf.kb = CULL_K * fmax3abs(rf.d.x, rf.d.y, rf.d.z);
+    rf.kdet = 8.0f * CULL_K * rf.a;
+    rf.oinf = fmax3abs(rf.o.x, rf.o.y, rf.o.z);
+    return rf;
+}
+__device__ __forceinline__ HitD no_hit() {
     HitD h;
     h.dist = DBL_MAX;
     h.pt = 0;
     h.slot = -1;
-    RayF rf;
-    if (MIXED) {
-        rf.o = F3((float)r.o.x, (float)r.o.y, (float)r.o.z);
-        rf.d = F3((float)r.d.x, (float)r.d.y, (float)r.d.z);
-        rf.a = fdot(rf.d, rf.d);
-        rf.kb = CULL_K * fmax3abs(rf.d.x, rf.d.y, rf.d.z);
-        rf.kdet = 8.0f * CULL_K * rf.a;
-        rf.oinf = fmax3abs(rf.o.x, rf.o.y, rf.o.z);
+    return h;
+}
+/* sphere s (wave-uniform index), exact, behind the MIXED per-lane fp32 cull */
+template <bool MIXED>
+__device__ __forceinline__ void sphere_by_index(const KParams& p, int s, const RayD& r,
+                                                const RayF& rf, HitD& h) {
+    if (MIXED && sphere_cull(p.s32[s >> 2].v[s & 3], rf)) return;
+    sphere_exact(p.s64[s >> 2].v[s & 3], s, r, h);
+}
+template <bool MIXED>
+__device__ __forceinline__ void walls_d(const KParams& p, const RayD& r, const RayF& rf, HitD& h) {
+    for (int w = 0; w < p.nW; ++w) {
+        if (MIXED && wall_cull(p.w32[w], rf)) continue;
+        wall_exact(p.w64[w], w, p, r, h);
     }
+}
+
+/* Nearest-first traversal of the wave-culled spheres (scenes of <= 256 spheres).
+ * The cull pass also gives each surviving sphere a lower bound on its hit distance,
+ * |C - apex| - r - rho (minus margins) <= |hit - o_i| for every live ray i.  Survivors are
+ * extracted in increasing bound order (one wave-min per step) and the traversal stops
+ * as soon as no live lane's best distance could be beaten (a tie still counts: the lower
+ * scene index wins it).  Walls are tested first so their distances already bound the
+ * spheres.  The per-lane tests are the exact ones, in a different order; with the
+ * order-independent tie rule the winner is the reference's. */
+constexpr int SORT_CHUNKS = 4;
+
+struct Survivors {
+    float dm[SORT_CHUNKS];  // per lane: bound of sphere (64*c + lane), +inf if culled
+};
+
+__device__ __forceinline__ Survivors cull_sorted(const KParams& p, const Cone& cn) {
+    Survivors sv;
+    const float inf = __builtin_inff();
+    const int lane = (int)(threadIdx.x & 63);
+#pragma unroll
+    for (int c = 0; c < SORT_CHUNKS; ++c) {
+        const int s = 64 * c + lane;
+        float dmin = inf;
+        if (s < p.nS) {
+            const float* S = p.s32[s >> 2].v[s & 3];
+            const f3 v = F3(S[0], S[1], S[2]) - cn.apex;
+            const float L2 = fdot(v, v);
+            const float R = S[3] + cn.rho +
+                            1e-4f * (1.0f + cn.scale + fmax3abs(S[0], S[1], S[2]) + S[3]);
+            bool keep = true;
+            float lb = 0.0f;
+            if (L2 > R * R) {
+                const float il = frsq(L2);
+                lb = fmaxf(0.0f, (L2 * il - R) * 0.9999f);
+                if (cn.on) {
+                    const float sa = fminf(R * il, 1.0f);
+                    const float ca = fsqrt(fmaxf(0.0f, 1.0f - sa * sa));
+                    keep = fdot(cn.u, v) * il >= cn.cos_t * ca - cn.sin_t * sa - 1e-4f;
+                }
+            }
+            if (keep) dmin = lb;
+        }
+        sv.dm[c] = dmin;
+    }
+    if (p.stats != nullptr && lane == 0) {
+        int kept = 0;
+#pragma unroll
+        for (int c = 0; c < SORT_CHUNKS; ++c) kept += __popcll(__ballot(sv.dm[c] < inf));
+        atomicAdd(p.stats + 0, 1ull);
+        atomicAdd(p.stats + 1, (unsigned long long)kept);
+        atomicAdd(p.stats + 2, (unsigned long long)p.nS);
+    }
+    return sv;
+}
+
+/* Extract the nearest surviving sphere: returns its index (wave-uniform) and bound, or -1
+ * when none is left; removes it from sv. */
+__device__ __forceinline__ int pop_nearest(Survivors& sv, float& bound) {
+    float local = sv.dm[0];
+    int cid = 0;
+#pragma unroll
+    for (int c = 1; c < SORT_CHUNKS; ++c)
+        if (sv.dm[c] < local) {
+            local = sv.dm[c];
+            cid = c;
+        }
+    const float g = wmin(local);
+    if (!(g < __builtin_inff())) return -1;
+    const uint64_t at = __ballot(local == g);
+    const int L = __builtin_ctzll(at);
+    const int c = __builtin_amdgcn_readlane(cid, L);
+    if ((int)(threadIdx.x & 63) == L) {
+#pragma unroll
+        for (int k = 0; k < SORT_CHUNKS; ++k)
+            if (k == c) sv.dm[k] = __builtin_inff();
+    }
+    bound = g;
+    return 64 * c + L;
+}
+
+template <bool MIXED>
+__device__ __forceinline__ HitD closest_hit_wave(const KParams& p, const RayD& r, bool alive) {
+    HitD h = no_hit();
+    RayF rf;
+    if (MIXED) rf = make_rayf(r);
+    if (alive) walls_d<MIXED>(p, r, rf, h);
+    const Cone cn = wave_cone(F3((float)r.o.x, (float)r.o.y, (float)r.o.z),
+                              F3((float)r.d.x, (float)r.d.y, (float)r.d.z), alive);
+    Survivors sv = cull_sorted(p, cn);
+    for (;;) {
+        float bound;
+        const int sidx = pop_nearest(sv, bound);
+        if (sidx < 0) break;
+        if (!__any(alive && (double)bound <= h.dist)) break;  // nothing left can win
+        if (alive && (double)bound <= h.dist) {
+            if (!(MIXED && sphere_cull(p.s32[sidx >> 2].v[sidx & 3], rf)))
+                sphere_exact<false>(p.s64[sidx >> 2].v[sidx & 3], sidx, r, h, &p);
+        }
+    }
+    return h;
+}
+
+/* Linear scan (no wave cull): groups of 4 spheres per scalar load. */
+template <bool MIXED>
+__device__ __forceinline__ HitD closest_hit_d(const KParams& p, const RayD& r) {
+    HitD h = no_hit();
+    RayF rf;
+    if (MIXED) rf = make_rayf(r);
     const int ng = (p.nS + 3) >> 2;
     for (int g = 0; g < ng; ++g) {
         if (MIXED) {
@@ -324,10 +565,7 @@ __device__ __forceinline__ HitD closest_hit_d(const KParams& p, const RayD& r) {
             }
         }
     }
-    for (int w = 0; w < p.nW; ++w) {
-        if (MIXED && wall_cull(p.w32[w], rf)) continue;
-        wall_exact(p.w64[w], w, p, r, h);
-    }
+    walls_d<MIXED>(p, r, rf, h);
     return h;
 }
 
@@ -417,7 +655,8 @@ __device__ __forceinline__ f3 tof(d3 v) { return F3((float)v.x, (float)v.y, (flo
 /* One pixel on the exact fp64 ray path.  COLOR64: colour arithmetic in fp64 too (F64 /
  * MIXED, the parity modes); otherwise in fp32 (PATH64). */
 template <bool MIXED, bool COLOR64, bool SUN, bool INT_EXP, int MAXD>
-__device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, int& segs) {
+__device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool alive,
+                                            int& segs) {
     using CT = typename std::conditional<COLOR64, double, float>::type;
     const d3 cpos = ld3(p.pos);
     const d3 pc = (ld3(p.tl) + ld3(p.dx) * (double)x) + ld3(p.dy) * (double)i;  // main.cpp:132
@@ -428,11 +667,36 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, int&
     CT st_k[MAXD];
     int st_m[MAXD];
     int n = 0;
-    d3 c64;
-    f3 c32;
+    d3 c64 = D3(0, 0, 0);
+    f3 c32 = F3(0.f, 0.f, 0.f);
+    // Converged bounce loop: lanes whose path ended stay (alive == false) so the wave can
+    // reduce over its live rays; k is wave-uniform.
     for (int k = 0;; ++k) {
+        if (!__any(alive)) break;
+        HitD h = no_hit();
+        if (p.wave_cull && p.nS <= 64 * SORT_CHUNKS) {
+            h = closest_hit_wave<MIXED>(p, r, alive);
+        } else if (p.wave_cull) {
+            const Cone cn = wave_cone(F3((float)r.o.x, (float)r.o.y, (float)r.o.z),
+                                      F3((float)r.d.x, (float)r.d.y, (float)r.d.z), alive);
+            RayF rf;
+            if (MIXED) rf = make_rayf(r);
+            for (int c0 = 0; c0 < p.nS; c0 += 64) {
+                uint64_t m = cull_chunk(p, cn, c0);
+                if (alive) {
+                    while (m) {
+                        const int sidx = c0 + __builtin_ctzll(m);
+                        m &= m - 1;
+                        sphere_by_index<MIXED>(p, sidx, r, rf, h);
+                    }
+                }
+            }
+            if (alive) walls_d<MIXED>(p, r, rf, h);
+        } else if (alive) {
+            h = closest_hit_d<MIXED>(p, r);
+        }
+        if (!alive) continue;
         ++segs;
-        const HitD h = closest_hit_d<MIXED>(p, r);
         const double rdl = rcp_refined(r.dlen);
         const d3 nv = div3(r.d, r.dlen, rdl);  // normalize(d); normalize(-d) == -nv
         if (h.slot < 0) {
@@ -445,7 +709,8 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, int&
                 c32 = F3(fmaf(tz, 0.14f - 0.36f, 0.36f), fmaf(tz, 0.21f - 0.45f, 0.45f),
                          fmaf(tz, 0.49f - 0.57f, 0.57f));
             }
-            break;
+            alive = false;
+            continue;
         }
         const d3 pos = r.o + r.d * h.dist;  // main.cpp:99 (sphere world distance used as t)
         d3 N;
@@ -472,7 +737,8 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, int&
                 c64 = local_color_d(m, s, ks, sun);
             else
                 c32 = local_color_f(m, s, ks, sun);
-            break;
+            alive = false;
+            continue;
         }
         st_s[k] = s;
         st_k[k] = ks;
@@ -503,8 +769,57 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, int&
 /* ------------------------------------------------------------------------ */
 /* fp32 throughput path                                                      */
 /* ------------------------------------------------------------------------ */
+/* fp32 sphere test (scaled form; det == 0 keeps scene.cpp:65's 2x distance).
+ * IN_ORDER as for sphere_exact. */
+template <bool IN_ORDER = true>
+__device__ __forceinline__ void sphere_f(const float* S, int s, f3 o, f3 d, float a, float ra,
+                                         float rl, float& best, float& bpt, int& slot,
+                                         const KParams* p = nullptr) {
+    const f3 oc = o - F3(S[0], S[1], S[2]);
+    const float bh = fdot(d, oc);
+    const float cq = fmaf(-S[3], S[3], fdot(oc, oc));
+    const float det = fmaf(bh, bh, -a * cq);
+    if (bh <= 0.0f && det >= 0.0f) {
+        const float num = -bh - fsqrt(det);
+        const float proj = (det == 0.0f) ? -2.0f * bh * ra : num * ra;
+        const float dist = proj * a * rl;  // proj * |d|
+        const bool ok = (det == 0.0f || num > 0.0f) && dist > 0.0f;
+        bool take = ok && dist < best;
+        if (!IN_ORDER && ok && !take && dist == best && slot >= 0)
+            take = scene_index(*p, s) < scene_index(*p, slot);
+        if (take) {
+            best = dist;
+            bpt = (det == 0.0f) ? -bh * ra : proj;
+            slot = s;
+        }
+    }
+}
+
+__device__ __forceinline__ void walls_f(const KParams& p, f3 o, f3 d, float& best, int& slot) {
+    for (int w = 0; w < p.nW; ++w) {
+        const Wall32& Wl = p.w32[w];
+        const f3 nw = F3(Wl.n[0], Wl.n[1], Wl.n[2]), P = F3(Wl.P[0], Wl.P[1], Wl.P[2]);
+        const float den = fdot(nw, d);
+        const float num = fdot(P - o, nw);
+        if (!((num > 0 && den > 0) || (num < 0 && den < 0))) continue;
+        const float t = num * frcp(den);
+        const f3 q = fmad3(d, t, o) - P;
+        const float px = fdot(q, F3(Wl.X[0], Wl.X[1], Wl.X[2]));
+        const float py = fdot(q, F3(Wl.Y[0], Wl.Y[1], Wl.Y[2]));
+        if (t > 0 && px >= 0 && px <= Wl.len && py >= 0 && py <= Wl.wid) {
+            bool take = t < best;
+            if (!take && t == best && slot >= 0) take = p.wall_j[w] < scene_index(p, slot);
+            if (take) {
+                best = t;
+                slot = p.nS + w;
+            }
+        }
+    }
+}
+
 template <bool SUN, int MAXD>
-__device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, int& segs) {
+__device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, bool alive,
+                                            int& segs) {
     const d3 pcd = (ld3(p.tl) + ld3(p.dx) * (double)x) + ld3(p.dy) * (double)i;
     const d3 dd = ld3(p.pos) - pcd;
     f3 o = F3((float)p.pos[0], (float)p.pos[1], (float)p.pos[2]);
@@ -515,57 +830,55 @@ __device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, int&
     float st_k[MAXD];
     int st_m[MAXD];
     int n = 0;
-    f3 c;
+    f3 c = F3(0.f, 0.f, 0.f);
     for (int k = 0;; ++k) {
-        ++segs;
+        if (!__any(alive)) break;
         const float a = fdot(d, d);
         const float ra = frcp(a);
         const float rl = frsq(a);
         float best = FLT_MAX, bpt = 0.0f;
         int slot = -1;
-        const int ng = (p.nS + 3) >> 2;
-        for (int g = 0; g < ng; ++g) {
-            const SphG32 G = p.s32[g];
+        if (p.wave_cull && p.nS <= 64 * SORT_CHUNKS) {
+            if (alive) walls_f(p, o, d, best, slot);
+            const Cone cn = wave_cone(o, d, alive);
+            Survivors sv = cull_sorted(p, cn);
+            for (;;) {
+                float bound;
+                const int sidx = pop_nearest(sv, bound);
+                if (sidx < 0) break;
+                if (!__any(alive && bound <= best)) break;
+                if (alive && bound <= best)
+                    sphere_f<false>(p.s32[sidx >> 2].v[sidx & 3], sidx, o, d, a, ra, rl, best,
+                                    bpt, slot, &p);
+            }
+        } else if (p.wave_cull) {
+            const Cone cn = wave_cone(o, d, alive);
+            for (int c0 = 0; c0 < p.nS; c0 += 64) {
+                uint64_t m = cull_chunk(p, cn, c0);
+                if (alive) {
+                    while (m) {
+                        const int sidx = c0 + __builtin_ctzll(m);
+                        m &= m - 1;
+                        sphere_f(p.s32[sidx >> 2].v[sidx & 3], sidx, o, d, a, ra, rl, best, bpt,
+                                 slot);
+                    }
+                }
+            }
+        } else if (alive) {
+            const int ng = (p.nS + 3) >> 2;
+            for (int g = 0; g < ng; ++g) {
+                const SphG32 G = p.s32[g];
 #pragma unroll
-            for (int kk = 0; kk < 4; ++kk) {
-                const int s = 4 * g + kk;
-                if (s >= p.nS) break;
-                const float* S = G.v[kk];
-                const f3 oc = o - F3(S[0], S[1], S[2]);
-                const float bh = fdot(d, oc);
-                const float cq = fmaf(-S[3], S[3], fdot(oc, oc));
-                const float det = fmaf(bh, bh, -a * cq);
-                const float num = -bh - fsqrt(fmaxf(det, 0.0f));
-                // b <= 0, det >= 0, positive root; det==0 keeps scene.cpp:65's 2x
-                float proj = num * ra;
-                proj = (det == 0.0f) ? -2.0f * bh * ra : proj;
-                const float dist = proj * a * rl;  // proj * |d|
-                if (bh <= 0.0f && det >= 0.0f && num > 0.0f && dist > 0.0f && dist < best) {
-                    best = dist;
-                    bpt = (det == 0.0f) ? -bh * ra : proj;
-                    slot = s;
+                for (int kk = 0; kk < 4; ++kk) {
+                    const int sidx = 4 * g + kk;
+                    if (sidx >= p.nS) break;
+                    sphere_f(G.v[kk], sidx, o, d, a, ra, rl, best, bpt, slot);
                 }
             }
         }
-        for (int w = 0; w < p.nW; ++w) {
-            const Wall32& Wl = p.w32[w];
-            const f3 nw = F3(Wl.n[0], Wl.n[1], Wl.n[2]), P = F3(Wl.P[0], Wl.P[1], Wl.P[2]);
-            const float den = fdot(nw, d);
-            const float num = fdot(P - o, nw);
-            if (!((num > 0 && den > 0) || (num < 0 && den < 0))) continue;
-            const float t = num * frcp(den);
-            const f3 q = fmad3(d, t, o) - P;
-            const float px = fdot(q, F3(Wl.X[0], Wl.X[1], Wl.X[2]));
-            const float py = fdot(q, F3(Wl.Y[0], Wl.Y[1], Wl.Y[2]));
-            if (t > 0 && px >= 0 && px <= Wl.len && py >= 0 && py <= Wl.wid) {
-                bool take = t < best;
-                if (!take && t == best && slot >= 0) take = p.wall_j[w] < scene_index(p, slot);
-                if (take) {
-                    best = t;
-                    slot = p.nS + w;
-                }
-            }
-        }
+        if (!alive) continue;
+        ++segs;
+        if (!(p.wave_cull && p.nS <= 64 * SORT_CHUNKS)) walls_f(p, o, d, best, slot);
         const f3 nv = d * rl;
         if (slot < 0) {
             if (d.z < 0.0f) {
@@ -575,7 +888,8 @@ __device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, int&
                 c = F3(fmaf(tz, 0.14f - 0.36f, 0.36f), fmaf(tz, 0.21f - 0.45f, 0.45f),
                        fmaf(tz, 0.49f - 0.57f, 0.57f));
             }
-            break;
+            alive = false;
+            continue;
         }
         const f3 pos = fmad3(d, best, o);
         f3 N;
@@ -587,27 +901,15 @@ __device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, int&
             N = F3(Wl.n[0], Wl.n[1], Wl.n[2]);
         }
         const DevMat& m = p.mat[slot];
-        const float kd = (float)m.kd, ks = (float)m.ks, ka = (float)m.ka, ex = (float)m.ex;
         const f3 nn = fnormalize(N);
-        const f3 ldir = fnormalize(-pos);
-        const float lamb = fmaxf(fdot(ldir, nn), 0.0f);
-        const float res = fmaxf(fdot(fnormalize(ldir - nv), nn), 0.0f);
-        const float s = fmaf(lamb, kd, fmaf(fpow(res, ex), ks, ka));
-        float ksun = 0.0f;
-        if (sun) {
-            const f3 sd = fnormalize(F3(.7f, .4f, .7f));
-            const float sa = fmaxf(fdot(sd, nn), 0.0f);
-            const float hs = fmaxf(fdot(fnormalize(sd - nv), nn), 0.0f);
-            ksun = fmaf(sa, kd, fpow(hs, ex) * ks);
-        }
+        const float2 sh = shade_f(m, pos, nn, nv, sun);
         if (k >= p.depth || k >= MAXD) {
-            const f3 col = F3((float)m.color[0], (float)m.color[1], (float)m.color[2]);
-            c = col * s;
-            if (sun) c = fmad3(F3(1.64f * col.x, 1.27f * col.y, 0.99f * col.z), ksun, c);
-            break;
+            c = local_color_f(m, sh.x, sh.y, sun);
+            alive = false;
+            continue;
         }
-        st_s[k] = s;
-        st_k[k] = ksun;
+        st_s[k] = sh.x;
+        st_k[k] = sh.y;
         st_m[k] = slot;
         n = k + 1;
         const float cc = 2.0f * fdot(nv, nn);
@@ -617,9 +919,7 @@ __device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, int&
     for (int q = MAXD - 1; q >= 0; --q) {
         if (q < n) {
             const DevMat& m = p.mat[st_m[q]];
-            const f3 col = F3((float)m.color[0], (float)m.color[1], (float)m.color[2]);
-            f3 L = col * st_s[q];
-            if (sun) L = fmad3(F3(1.64f * col.x, 1.27f * col.y, 0.99f * col.z), st_k[q], L);
+            const f3 L = local_color_f(m, st_s[q], st_k[q], sun);
             const float km = (float)m.km;
             c = F3(fmaf(km, c.x - L.x, L.x), fmaf(km, c.y - L.y, L.y), fmaf(km, c.z - L.z, L.z));
         }
@@ -682,18 +982,16 @@ k_trace(KParams p) {
     const int x = blockIdx.x * TILE_W + (wave & 1) * 8 + (lane & 7);
     const int r = blockIdx.y * TILE_H + (wave >> 1) * 8 + (lane >> 3);
     const bool valid = x < p.W && r < p.nrows;
+    const int i = p.row0 + r;
     int segs = 0;
-    if (valid) {
-        const int i = p.row0 + r;
-        if (PREC == PREC_F32) {
-            const f3 c = trace_pixel_f<SUN, MAXD>(p, x, i, segs);
-            store_pixel(p, r, x, c.x, c.y, c.z);
-        } else {
-            const d3 c =
-                trace_pixel_d<PREC == PREC_MIXED, PREC != PREC_PATH64, SUN, INT_EXP, MAXD>(
-                    p, x, i, segs);
-            store_pixel(p, r, x, c.x, c.y, c.z);
-        }
+    // every lane runs the (converged) bounce loop; only valid lanes trace and store
+    if (PREC == PREC_F32) {
+        const f3 c = trace_pixel_f<SUN, MAXD>(p, x, i, valid, segs);
+        if (valid) store_pixel(p, r, x, c.x, c.y, c.z);
+    } else {
+        const d3 c = trace_pixel_d<PREC == PREC_MIXED, PREC != PREC_PATH64, SUN, INT_EXP, MAXD>(
+            p, x, i, valid, segs);
+        if (valid) store_pixel(p, r, x, c.x, c.y, c.z);
     }
     count_segments(p, segs);
 }

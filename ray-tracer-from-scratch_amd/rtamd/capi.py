@@ -43,6 +43,9 @@ RT_OUT_RGBA8 = 2
 
 RT_FLAG_SUN = 1
 
+RT_OPT_WAVE_CULL_MIN_SPHERES = 1
+RT_OPT_STATS_DEVICE_PTR = 2
+
 
 class rt_material(C.Structure):
     _fields_ = [
@@ -92,6 +95,7 @@ SIGNATURES = [
     ("rt_last_hip_error", C.c_char_p, [C.c_void_p]),
     ("rt_capi_version", C.c_int, []),
     ("rt_set_scene", C.c_int, [C.c_void_p, C.POINTER(rt_prim), C.c_int32]),
+    ("rt_set_option", C.c_int, [C.c_void_p, C.c_int32, C.c_int64]),
     ("rt_render", C.c_int,
      [C.c_void_p, C.POINTER(rt_camera), C.c_int32, C.c_int32, C.c_int32, C.c_int32,
       C.c_uint32, C.c_int32, C.c_void_p, C.c_int32, C.POINTER(rt_stats)]),
@@ -212,6 +216,9 @@ class Renderer:
         arr = (rt_prim * len(prims))(*prims)
         self._prims = arr
         check(self.lib.rt_set_scene(self.ctx, arr, len(prims)), self.ctx)
+
+    def set_option(self, option: int, value: int) -> None:
+        check(self.lib.rt_set_option(self.ctx, option, value), self.ctx)
 
     def selftest(self, test: int, n: int, seed: int = 1) -> int:
         bad = C.c_uint64()

@@ -334,3 +334,31 @@ def test_non_integer_specular_exponent(rend, oracle):
         img, _, cam = render(rend, sc, 64, 36, 5, prec)
         o64, _, _, sig = oracle.render(scenes.to_prims(sc), cam, 5, want_sig=True)
         check_f64(img, o64, sig, what=("nonint", prec))
+
+
+# ---------------------------------------------------------------- wave cull
+@pytest.mark.parametrize("prec", [capi.RT_PREC_F64, capi.RT_PREC_MIXED, capi.RT_PREC_PATH64,
+                                  capi.RT_PREC_F32])
+def test_wave_cull_is_output_invariant(rend, prec):
+    """The wave-cooperative cull only skips spheres no live ray of the wave can hit: frames
+    with it forced on and forced off are bitwise identical, for every precision."""
+    rng = np.random.default_rng(11)
+    try:
+        # sizes cover the nearest-first traversal (<= 256 spheres) and the chunked one
+        for trial, ns in enumerate((20, 97, 256, 300)):
+            sc = scenes.synthetic_scene(ns, int(rng.integers(0, 7)),
+                                        seed=int(rng.integers(1 << 30)))
+            rend.set_scene(scenes.to_prims(sc))
+            pos = rng.uniform([-1, -3, -1], [5, 3, 2])
+            cam = capi.camera_init(pos, pos + rng.normal(size=3), (0, 0, -1),
+                                   float(rng.uniform(40, 110)), 16 / 9, 192.0)
+            depth = int(rng.integers(2, 9))
+            imgs = []
+            for cull in (0, 2**31 - 1):
+                rend.set_option(capi.RT_OPT_WAVE_CULL_MIN_SPHERES, cull)
+                img, st = rend.render(cam, depth, prec, 0, capi.RT_OUT_RGB_F64, count_segments=True)
+                imgs.append((img, st.segments))
+            assert imgs[0][1] == imgs[1][1], trial
+            assert np.array_equal(imgs[0][0].view(np.uint64), imgs[1][0].view(np.uint64)), trial
+    finally:
+        rend.set_option(capi.RT_OPT_WAVE_CULL_MIN_SPHERES, 24)

@@ -26,8 +26,12 @@ rc=$?; echo "bench rc=$rc"; cat "$OUT/bench.json"; tail -5 "$OUT/bench.err"
 
 if [ "${SWEEP:-1}" = 1 ]; then
   step sweep
-  timeout -k 10 300 python tools/sweep.py > "$OUT/sweep.jsonl" 2> "$OUT/sweep.err"
+  timeout -k 10 300 python tools/sweep.py ${SWEEP_ARGS:-} > "$OUT/sweep.jsonl" 2> "$OUT/sweep.err"
   rc=$?; echo "sweep rc=$rc"; cat "$OUT/sweep.jsonl"
+  if [ $rc -eq 0 ] && [ -n "${SWEEP2_ARGS:-}" ]; then
+    timeout -k 10 300 python tools/sweep.py ${SWEEP2_ARGS} > "$OUT/sweep2.jsonl" 2>> "$OUT/sweep.err"
+    rc=$?; echo "sweep2 rc=$rc"; cat "$OUT/sweep2.jsonl"
+  fi
   [ $rc -eq 0 ] || exit $rc
 fi
 

@@ -21,12 +21,18 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--sun", action="store_true")
+    ap.add_argument("--cull", default="default", help="wave-cull min spheres: default|always|never|N")
     args = ap.parse_args()
     import torch
     dev = torch.device("cuda", 0)
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     rend = capi.Renderer(0)
+    cull = {"default": None, "always": 0, "never": 2**31 - 1}.get(args.cull, None)
+    if cull is None and args.cull != "default":
+        cull = int(args.cull)
+    if cull is not None:
+        rend.set_option(capi.RT_OPT_WAVE_CULL_MIN_SPHERES, cull)
     flags = capi.RT_FLAG_SUN if args.sun else 0
     rows = []
     for cname in args.configs.split(","):
@@ -58,11 +64,20 @@ def main():
                 e1.record(stream)
                 torch.cuda.synchronize()
                 times[p].append(e0.elapsed_time(e1) / args.reps)
+        # diagnostic: cull selectivity (one extra launch with counters on)
+        st = torch.zeros(3, dtype=torch.int64, device=dev)
+        rend.set_option(capi.RT_OPT_STATS_DEVICE_PTR, st.data_ptr())
+        rend.render_device(cam, cfg.depth, out.data_ptr(), capi.PRECISIONS[precs[0]], flags, 0,
+                           stream=stream.cuda_stream)
+        torch.cuda.synchronize()
+        rend.set_option(capi.RT_OPT_STATS_DEVICE_PTR, 0)
+        culls, kept, considered = (int(v) for v in st.tolist())
         for p in precs:
             ms = min(times[p])
-            r = dict(config=cname, precision=p, ms_min=round(ms, 4),
+            r = dict(config=cname, precision=p, cull=args.cull, ms_min=round(ms, 4),
                      ms_med=round(sorted(times[p])[len(times[p]) // 2], 4), segments=segs,
-                     grays=round(segs / (ms * 1e-3) / 1e9, 3))
+                     grays=round(segs / (ms * 1e-3) / 1e9, 3), culls=culls,
+                     kept_frac=round(kept / considered, 4) if considered else None)
             rows.append(r)
             print(json.dumps(r), flush=True)
     rend.close()
