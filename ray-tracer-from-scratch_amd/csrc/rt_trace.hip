@@ -47,6 +47,10 @@
 
 #include "rt_device.h"
 
+#ifndef RT_WALLS_FIRST
+#define RT_WALLS_FIRST 1
+#endif
+
 namespace rt {
 
 /* ------------------------------------------------------------------------ */
@@ -165,6 +169,7 @@ __device__ __forceinline__ d3 sun_direction() { return D3(.7, .4, .7); }
 /* Largest bounce count compiled: the register stack is sized per instantiation. */
 constexpr int MAXD_SMALL = 4;
 constexpr int MAXD_MID = 8;
+constexpr int MAXD_REF = 10;  // rt_scene's default recursion depth (main.cpp:89)
 constexpr int MAXD_LARGE = 16;
 
 /* ------------------------------------------------------------------------ */
@@ -344,6 +349,12 @@ __device__ __forceinline__ float wmax(float v) {
     return fmaxf(fmaxf(lane_f(v, 0), lane_f(v, 16)), fmaxf(lane_f(v, 32), lane_f(v, 48)));
 }
 __device__ __forceinline__ float uni(float v) { return v; }  // reductions are already scalar
+__device__ __forceinline__ double lane_d(double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffff), l);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
 
 struct Cone {
     f3 apex;
@@ -372,20 +383,36 @@ __device__ __forceinline__ Cone wave_cone(f3 o, f3 d, bool alive) {
     return c;
 }
 
-/* Ballot of the spheres in [c0, c0+64) that may be hit by a live ray of the wave. */
-__device__ __forceinline__ uint64_t cull_chunk_raw(const KParams& p, const Cone& cn, int c0) {
+/* Cull pass over spheres [c0, c0+64): lane l tests sphere c0 + l.  Returns the ballot of
+ * survivors; *lb receives (in lane l) a lower bound on sphere c0+l's hit distance for any
+ * live ray of the wave: |hit - o_i| >= |C - o_i| - r >= |C - apex| - rho - r. */
+struct SphRec {
+    float f[4];   // fp32 {cx, cy, cz, r} of sphere c0 + lane
+    double d[4];  // fp64 {cx, cy, cz, r^2} (WANT64 only)
+};
+template <bool WANT64>
+__device__ __forceinline__ uint64_t cull_chunk(const KParams& p, const Cone& cn, int c0,
+                                               float* lb, SphRec& rec) {
     const int s = c0 + (int)(threadIdx.x & 63);
     bool keep = false;
+    float bound = 0.0f;
     if (s < p.nS) {
         keep = true;
-        if (cn.on) {
-            const float* S = p.s32[s >> 2].v[s & 3];
-            const f3 v = F3(S[0], S[1], S[2]) - cn.apex;
-            const float L2 = fdot(v, v);
-            const float R = S[3] + cn.rho +
-                            1e-4f * (1.0f + cn.scale + fmax3abs(S[0], S[1], S[2]) + S[3]);
-            if (L2 > R * R) {  // apex outside the inflated ball
-                const float il = frsq(L2);
+        const float* S = p.s32[s >> 2].v[s & 3];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) rec.f[k] = S[k];
+        if (WANT64) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) rec.d[k] = p.s64[s >> 2].v[s & 3][k];
+        }
+        const f3 v = F3(S[0], S[1], S[2]) - cn.apex;
+        const float L2 = fdot(v, v);
+        const float R = S[3] + cn.rho +
+                        1e-4f * (1.0f + cn.scale + fmax3abs(S[0], S[1], S[2]) + S[3]);
+        if (L2 > R * R) {  // apex outside the inflated ball
+            const float il = frsq(L2);
+            bound = fmaxf(0.0f, (L2 * il - R) * 0.9999f);
+            if (cn.on) {
                 const float sa = fminf(R * il, 1.0f);
                 const float ca = fsqrt(fmaxf(0.0f, 1.0f - sa * sa));
                 const float cphi = fdot(cn.u, v) * il;
@@ -393,12 +420,9 @@ __device__ __forceinline__ uint64_t cull_chunk_raw(const KParams& p, const Cone&
             }
         }
     }
-    return __ballot(keep);
-}
-/* ... plus the optional diagnostic counters (KParams::stats: [0] culls, [1] spheres kept,
- * [2] spheres considered) — one lane, one atomic each, only when stats are requested. */
-__device__ __forceinline__ uint64_t cull_chunk(const KParams& p, const Cone& cn, int c0) {
-    const uint64_t m = cull_chunk_raw(p, cn, c0);
+    *lb = bound;
+    const uint64_t m = __ballot(keep);
+    // diagnostics (KParams::stats: [0] cull passes, [1] spheres kept, [2] spheres considered)
     if (p.stats != nullptr && (threadIdx.x & 63) == 0) {
         const int nin = p.nS - c0 < 64 ? p.nS - c0 : 64;
         atomicAdd(p.stats + 0, 1ull);
@@ -438,107 +462,6 @@ __device__ __forceinline__ void walls_d(const KParams& p, const RayD& r, const R
         if (MIXED && wall_cull(p.w32[w], rf)) continue;
         wall_exact(p.w64[w], w, p, r, h);
     }
-}
-
-/* Nearest-first traversal of the wave-culled spheres (scenes of <= 256 spheres).
- * The cull pass also gives each surviving sphere a lower bound on its hit distance,
- * |C - apex| - r - rho (minus margins) <= |hit - o_i| for every live ray i.  Survivors are
- * extracted in increasing bound order (one wave-min per step) and the traversal stops
- * as soon as no live lane's best distance could be beaten (a tie still counts: the lower
- * scene index wins it).  Walls are tested first so their distances already bound the
- * spheres.  The per-lane tests are the exact ones, in a different order; with the
- * order-independent tie rule the winner is the reference's. */
-constexpr int SORT_CHUNKS = 4;
-
-struct Survivors {
-    float dm[SORT_CHUNKS];  // per lane: bound of sphere (64*c + lane), +inf if culled
-};
-
-__device__ __forceinline__ Survivors cull_sorted(const KParams& p, const Cone& cn) {
-    Survivors sv;
-    const float inf = __builtin_inff();
-    const int lane = (int)(threadIdx.x & 63);
-#pragma unroll
-    for (int c = 0; c < SORT_CHUNKS; ++c) {
-        const int s = 64 * c + lane;
-        float dmin = inf;
-        if (s < p.nS) {
-            const float* S = p.s32[s >> 2].v[s & 3];
-            const f3 v = F3(S[0], S[1], S[2]) - cn.apex;
-            const float L2 = fdot(v, v);
-            const float R = S[3] + cn.rho +
-                            1e-4f * (1.0f + cn.scale + fmax3abs(S[0], S[1], S[2]) + S[3]);
-            bool keep = true;
-            float lb = 0.0f;
-            if (L2 > R * R) {
-                const float il = frsq(L2);
-                lb = fmaxf(0.0f, (L2 * il - R) * 0.9999f);
-                if (cn.on) {
-                    const float sa = fminf(R * il, 1.0f);
-                    const float ca = fsqrt(fmaxf(0.0f, 1.0f - sa * sa));
-                    keep = fdot(cn.u, v) * il >= cn.cos_t * ca - cn.sin_t * sa - 1e-4f;
-                }
-            }
-            if (keep) dmin = lb;
-        }
-        sv.dm[c] = dmin;
-    }
-    if (p.stats != nullptr && lane == 0) {
-        int kept = 0;
-#pragma unroll
-        for (int c = 0; c < SORT_CHUNKS; ++c) kept += __popcll(__ballot(sv.dm[c] < inf));
-        atomicAdd(p.stats + 0, 1ull);
-        atomicAdd(p.stats + 1, (unsigned long long)kept);
-        atomicAdd(p.stats + 2, (unsigned long long)p.nS);
-    }
-    return sv;
-}
-
-/* Extract the nearest surviving sphere: returns its index (wave-uniform) and bound, or -1
- * when none is left; removes it from sv. */
-__device__ __forceinline__ int pop_nearest(Survivors& sv, float& bound) {
-    float local = sv.dm[0];
-    int cid = 0;
-#pragma unroll
-    for (int c = 1; c < SORT_CHUNKS; ++c)
-        if (sv.dm[c] < local) {
-            local = sv.dm[c];
-            cid = c;
-        }
-    const float g = wmin(local);
-    if (!(g < __builtin_inff())) return -1;
-    const uint64_t at = __ballot(local == g);
-    const int L = __builtin_ctzll(at);
-    const int c = __builtin_amdgcn_readlane(cid, L);
-    if ((int)(threadIdx.x & 63) == L) {
-#pragma unroll
-        for (int k = 0; k < SORT_CHUNKS; ++k)
-            if (k == c) sv.dm[k] = __builtin_inff();
-    }
-    bound = g;
-    return 64 * c + L;
-}
-
-template <bool MIXED>
-__device__ __forceinline__ HitD closest_hit_wave(const KParams& p, const RayD& r, bool alive) {
-    HitD h = no_hit();
-    RayF rf;
-    if (MIXED) rf = make_rayf(r);
-    if (alive) walls_d<MIXED>(p, r, rf, h);
-    const Cone cn = wave_cone(F3((float)r.o.x, (float)r.o.y, (float)r.o.z),
-                              F3((float)r.d.x, (float)r.d.y, (float)r.d.z), alive);
-    Survivors sv = cull_sorted(p, cn);
-    for (;;) {
-        float bound;
-        const int sidx = pop_nearest(sv, bound);
-        if (sidx < 0) break;
-        if (!__any(alive && (double)bound <= h.dist)) break;  // nothing left can win
-        if (alive && (double)bound <= h.dist) {
-            if (!(MIXED && sphere_cull(p.s32[sidx >> 2].v[sidx & 3], rf)))
-                sphere_exact<false>(p.s64[sidx >> 2].v[sidx & 3], sidx, r, h, &p);
-        }
-    }
-    return h;
 }
 
 /* Linear scan (no wave cull): groups of 4 spheres per scalar load. */
@@ -654,7 +577,7 @@ __device__ __forceinline__ f3 tof(d3 v) { return F3((float)v.x, (float)v.y, (flo
 
 /* One pixel on the exact fp64 ray path.  COLOR64: colour arithmetic in fp64 too (F64 /
  * MIXED, the parity modes); otherwise in fp32 (PATH64). */
-template <bool MIXED, bool COLOR64, bool SUN, bool INT_EXP, int MAXD>
+template <bool MIXED, bool COLOR64, bool SUN, bool INT_EXP, bool CULL, int MAXD>
 __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool alive,
                                             int& segs) {
     using CT = typename std::conditional<COLOR64, double, float>::type;
@@ -674,24 +597,37 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
     for (int k = 0;; ++k) {
         if (!__any(alive)) break;
         HitD h = no_hit();
-        if (p.wave_cull && p.nS <= 64 * SORT_CHUNKS) {
-            h = closest_hit_wave<MIXED>(p, r, alive);
-        } else if (p.wave_cull) {
-            const Cone cn = wave_cone(F3((float)r.o.x, (float)r.o.y, (float)r.o.z),
-                                      F3((float)r.d.x, (float)r.d.y, (float)r.d.z), alive);
+        if (CULL) {
+            // walls first: their distances then bound the sphere tests
             RayF rf;
             if (MIXED) rf = make_rayf(r);
+            if (RT_WALLS_FIRST && alive) walls_d<MIXED>(p, r, rf, h);
+            const Cone cn = wave_cone(F3((float)r.o.x, (float)r.o.y, (float)r.o.z),
+                                      F3((float)r.d.x, (float)r.d.y, (float)r.d.z), alive);
             for (int c0 = 0; c0 < p.nS; c0 += 64) {
-                uint64_t m = cull_chunk(p, cn, c0);
-                if (alive) {
-                    while (m) {
-                        const int sidx = c0 + __builtin_ctzll(m);
-                        m &= m - 1;
-                        sphere_by_index<MIXED>(p, sidx, r, rf, h);
+                float lb;
+                SphRec rec;
+                uint64_t m = cull_chunk<true>(p, cn, c0, &lb, rec);
+                // survivors in index order; each record comes out of the testing lane's
+                // registers (v_readlane), no memory round trip
+                while (m) {
+                    const int l = __builtin_ctzll(m);
+                    m &= m - 1;
+                    const double bound = (double)lane_f(lb, l);
+                    // exact skip: the sphere's distance is >= bound > this lane's best
+                    if (alive && bound <= h.dist) {
+                        const int sidx = c0 + l;
+                        const float Sf[4] = {lane_f(rec.f[0], l), lane_f(rec.f[1], l),
+                                             lane_f(rec.f[2], l), lane_f(rec.f[3], l)};
+                        if (!(MIXED && sphere_cull(Sf, rf))) {
+                            const double Sd[4] = {lane_d(rec.d[0], l), lane_d(rec.d[1], l),
+                                                  lane_d(rec.d[2], l), lane_d(rec.d[3], l)};
+                            sphere_exact<false>(Sd, sidx, r, h, &p);
+                        }
                     }
                 }
             }
-            if (alive) walls_d<MIXED>(p, r, rf, h);
+            if (!RT_WALLS_FIRST && alive) walls_d<MIXED>(p, r, rf, h);
         } else if (alive) {
             h = closest_hit_d<MIXED>(p, r);
         }
@@ -817,7 +753,7 @@ __device__ __forceinline__ void walls_f(const KParams& p, f3 o, f3 d, float& bes
     }
 }
 
-template <bool SUN, int MAXD>
+template <bool SUN, bool CULL, int MAXD>
 __device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, bool alive,
                                             int& segs) {
     const d3 pcd = (ld3(p.tl) + ld3(p.dx) * (double)x) + ld3(p.dy) * (double)i;
@@ -838,32 +774,25 @@ __device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, bool
         const float rl = frsq(a);
         float best = FLT_MAX, bpt = 0.0f;
         int slot = -1;
-        if (p.wave_cull && p.nS <= 64 * SORT_CHUNKS) {
-            if (alive) walls_f(p, o, d, best, slot);
-            const Cone cn = wave_cone(o, d, alive);
-            Survivors sv = cull_sorted(p, cn);
-            for (;;) {
-                float bound;
-                const int sidx = pop_nearest(sv, bound);
-                if (sidx < 0) break;
-                if (!__any(alive && bound <= best)) break;
-                if (alive && bound <= best)
-                    sphere_f<false>(p.s32[sidx >> 2].v[sidx & 3], sidx, o, d, a, ra, rl, best,
-                                    bpt, slot, &p);
-            }
-        } else if (p.wave_cull) {
+        if (CULL) {
+            if (RT_WALLS_FIRST && alive) walls_f(p, o, d, best, slot);
             const Cone cn = wave_cone(o, d, alive);
             for (int c0 = 0; c0 < p.nS; c0 += 64) {
-                uint64_t m = cull_chunk(p, cn, c0);
+                float lb;
+                SphRec rec;
+                uint64_t m = cull_chunk<false>(p, cn, c0, &lb, rec);
+                // (a distance skip costs more than it saves at fp32 test prices: A/B)
                 if (alive) {
                     while (m) {
-                        const int sidx = c0 + __builtin_ctzll(m);
+                        const int l = __builtin_ctzll(m);
                         m &= m - 1;
-                        sphere_f(p.s32[sidx >> 2].v[sidx & 3], sidx, o, d, a, ra, rl, best, bpt,
-                                 slot);
+                        const float Sf[4] = {lane_f(rec.f[0], l), lane_f(rec.f[1], l),
+                                             lane_f(rec.f[2], l), lane_f(rec.f[3], l)};
+                        sphere_f<false>(Sf, c0 + l, o, d, a, ra, rl, best, bpt, slot, &p);
                     }
                 }
             }
+            if (!RT_WALLS_FIRST && alive) walls_f(p, o, d, best, slot);
         } else if (alive) {
             const int ng = (p.nS + 3) >> 2;
             for (int g = 0; g < ng; ++g) {
@@ -878,7 +807,7 @@ __device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, bool
         }
         if (!alive) continue;
         ++segs;
-        if (!(p.wave_cull && p.nS <= 64 * SORT_CHUNKS)) walls_f(p, o, d, best, slot);
+        if (!CULL) walls_f(p, o, d, best, slot);
         const f3 nv = d * rl;
         if (slot < 0) {
             if (d.z < 0.0f) {
@@ -965,17 +894,27 @@ __device__ __forceinline__ void count_segments(const KParams& p, int segs) {
 
 /* Occupancy target per instantiation (waves per SIMD; MI355X_MICROARCH.md: <= 128 VGPRs
  * for 4, <= 96 for 5).  The fp64-colour paths carry the most state. */
-template <int PREC, bool SUN, bool INT_EXP, int MAXD>
+template <int PREC, bool SUN, bool INT_EXP, bool CULL, int MAXD>
 constexpr int waves_per_eu() {
-    if (PREC == PREC_F32) return 5;
-    if (PREC == PREC_PATH64) return 4;
-    const int w = INT_EXP ? (SUN ? 3 : 4) : (SUN ? 2 : 3);
-    return (MAXD >= 16 && w > 2) ? w - 1 : w;
+    // The register stack costs 2-5 VGPRs per level and the cull's per-lane records ~12, so
+    // the target steps down with depth tier and cull.  Checked with `make asm`
+    // (ScratchSize 0 for every no-sun integer-exponent variant; the rare sun +
+    // non-integer-exponent deep fp64 variants run at 2 waves and may spill a little).
+    const int tier = MAXD >= 16 ? 2 : (MAXD >= 10 ? 1 : 0);
+    int w;
+    if (PREC == PREC_F32)
+        w = 5 - (tier > 0 ? 1 : 0) - ((SUN && tier == 2) ? 1 : 0);
+    else if (PREC == PREC_PATH64)
+        w = 4 - (tier == 2 ? 1 : 0) - ((SUN && tier > 0) ? 1 : 0);
+    else
+        w = (INT_EXP ? (SUN ? 3 : 4) : (SUN ? 2 : 3)) - (tier > 0 ? 1 : 0) -
+            ((CULL && MAXD >= 8) ? 1 : 0);
+    return w < 2 ? 2 : w;
 }
 
-template <int PREC, bool SUN, bool INT_EXP, int MAXD>
+template <int PREC, bool SUN, bool INT_EXP, bool CULL, int MAXD>
 __global__ void __launch_bounds__(BLOCK)
-__attribute__((amdgpu_waves_per_eu(waves_per_eu<PREC, SUN, INT_EXP, MAXD>(), 8)))
+__attribute__((amdgpu_waves_per_eu(waves_per_eu<PREC, SUN, INT_EXP, CULL, MAXD>(), 8)))
 k_trace(KParams p) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -986,38 +925,49 @@ k_trace(KParams p) {
     int segs = 0;
     // every lane runs the (converged) bounce loop; only valid lanes trace and store
     if (PREC == PREC_F32) {
-        const f3 c = trace_pixel_f<SUN, MAXD>(p, x, i, valid, segs);
+        const f3 c = trace_pixel_f<SUN, CULL, MAXD>(p, x, i, valid, segs);
         if (valid) store_pixel(p, r, x, c.x, c.y, c.z);
     } else {
-        const d3 c = trace_pixel_d<PREC == PREC_MIXED, PREC != PREC_PATH64, SUN, INT_EXP, MAXD>(
-            p, x, i, valid, segs);
+        const d3 c =
+            trace_pixel_d<PREC == PREC_MIXED, PREC != PREC_PATH64, SUN, INT_EXP, CULL, MAXD>(
+                p, x, i, valid, segs);
         if (valid) store_pixel(p, r, x, c.x, c.y, c.z);
     }
     count_segments(p, segs);
 }
 
-template <int PREC, bool SUN, bool INT_EXP>
-static hipError_t launch_prec(const KParams& p, dim3 grid, hipStream_t st) {
+template <int PREC, bool SUN, bool INT_EXP, bool CULL>
+static hipError_t launch_depth(const KParams& p, dim3 grid, hipStream_t st) {
     if (p.depth <= MAXD_SMALL)
-        hipLaunchKernelGGL((k_trace<PREC, SUN, INT_EXP, MAXD_SMALL>), grid, dim3(BLOCK), 0, st, p);
+        hipLaunchKernelGGL((k_trace<PREC, SUN, INT_EXP, CULL, MAXD_SMALL>), grid, dim3(BLOCK), 0,
+                           st, p);
     else if (p.depth <= MAXD_MID)
-        hipLaunchKernelGGL((k_trace<PREC, SUN, INT_EXP, MAXD_MID>), grid, dim3(BLOCK), 0, st, p);
+        hipLaunchKernelGGL((k_trace<PREC, SUN, INT_EXP, CULL, MAXD_MID>), grid, dim3(BLOCK), 0, st,
+                           p);
+    else if (p.depth <= MAXD_REF)
+        hipLaunchKernelGGL((k_trace<PREC, SUN, INT_EXP, CULL, MAXD_REF>), grid, dim3(BLOCK), 0, st,
+                           p);
     else
-        hipLaunchKernelGGL((k_trace<PREC, SUN, INT_EXP, MAXD_LARGE>), grid, dim3(BLOCK), 0, st, p);
+        hipLaunchKernelGGL((k_trace<PREC, SUN, INT_EXP, CULL, MAXD_LARGE>), grid, dim3(BLOCK), 0,
+                           st, p);
     return hipGetLastError();
+}
+template <int PREC, bool SUN, bool INT_EXP>
+static hipError_t launch_cull(const KParams& p, dim3 grid, hipStream_t st) {
+    return p.wave_cull ? launch_depth<PREC, SUN, INT_EXP, true>(p, grid, st)
+                       : launch_depth<PREC, SUN, INT_EXP, false>(p, grid, st);
 }
 template <int PREC>
 static hipError_t launch_prec(const KParams& p, dim3 grid, hipStream_t st) {
-    // the fp32 colour paths never use the fp64 pow: one variant
     if constexpr (PREC == PREC_F64 || PREC == PREC_MIXED) {
         if (p.flags & FLAG_SUN)
-            return p.int_exp ? launch_prec<PREC, true, true>(p, grid, st)
-                             : launch_prec<PREC, true, false>(p, grid, st);
-        return p.int_exp ? launch_prec<PREC, false, true>(p, grid, st)
-                         : launch_prec<PREC, false, false>(p, grid, st);
+            return p.int_exp ? launch_cull<PREC, true, true>(p, grid, st)
+                             : launch_cull<PREC, true, false>(p, grid, st);
+        return p.int_exp ? launch_cull<PREC, false, true>(p, grid, st)
+                         : launch_cull<PREC, false, false>(p, grid, st);
     } else {
-        return (p.flags & FLAG_SUN) ? launch_prec<PREC, true, true>(p, grid, st)
-                                    : launch_prec<PREC, false, true>(p, grid, st);
+        return (p.flags & FLAG_SUN) ? launch_cull<PREC, true, true>(p, grid, st)
+                                    : launch_cull<PREC, false, true>(p, grid, st);
     }
 }
 

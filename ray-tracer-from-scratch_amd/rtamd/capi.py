@@ -137,6 +137,8 @@ def load(path: str | None = None) -> C.CDLL:
             f"{p} not built: run `make -C ray-tracer-from-scratch_amd` (or __graft_entry__.build())")
     lib = C.CDLL(p)
     for name, res, args in SIGNATURES:
+        if path is not None and not hasattr(lib, name):
+            continue  # an older build loaded side by side (tools/ab.py)
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
