@@ -32,7 +32,15 @@ from rtamd import capi, scenes  # noqa: E402
 
 METRIC = "Mrays/sec + ms/frame at 1920×1080 depth=4; 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
-VALU_PEAK_TFLOPS = {"f32": 157.3, "mixed": 157.3, "f64": 78.6}   # vector peaks (spec)
+VALU_PEAK_TFLOPS = {"f32": 157.3, "mixed": 157.3, "path64": 157.3, "f64": 78.6}  # spec
+DTYPE = {"f64": "f64", "mixed": "f64", "path64": "f64+f32", "f32": "f32"}
+PARITY = {  # what each precision guarantees vs the reference (tests/test_gpu_parity.py)
+    "f64": "per-pixel |delta| <= 1e-12 vs the reference's fp64 frames",
+    "mixed": "bit-identical to f64",
+    "path64": "exact fp64 ray paths (hits, normals, reflections); fp32 colour: every pixel "
+              "within 2e-5 of the reference, no discontinuity flips",
+    "f32": "|delta| <= 1e-4 on >= 99.5% of pixels at depth <= 4 (flips at discontinuities)",
+}
 
 
 def flop_per_segment(n_sph: int, n_wall: int) -> int:
@@ -92,11 +100,12 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c2", choices=sorted(scenes.CONFIGS))
-    ap.add_argument("--precision", default="mixed", choices=sorted(capi.PRECISIONS))
+    ap.add_argument("--precision", default="path64", choices=sorted(capi.PRECISIONS))
     ap.add_argument("--mode", default="frames", choices=["frames", "tiled"])
     ap.add_argument("--sun", action="store_true", help="build-defined sun term (off = parity)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-sweep", action="store_true", help="skip the per-precision kernel sweep")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
 
@@ -203,6 +212,24 @@ def main() -> int:
     torch.cuda.synchronize(dev)
     kernel_ms = ek0.elapsed_time(ek1) / nk
 
+    sweep = {}
+    if rank == 0 and not args.no_sweep:
+        for pname, pc in capi.PRECISIONS.items():
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            rend.render_device(cam, depth, out.data_ptr(), pc, flags, capi.RT_OUT_RGB_F32,
+                               row0=row0, nrows=nrows, stream=stream.cuda_stream)
+            e0.record(stream)
+            for _ in range(nk):
+                rend.render_device(cam, depth, out.data_ptr(), pc, flags, capi.RT_OUT_RGB_F32,
+                                   row0=row0, nrows=nrows, stream=stream.cuda_stream)
+            e1.record(stream)
+            torch.cuda.synchronize(dev)
+            kms = e0.elapsed_time(e1) / nk
+            sweep[pname] = {"kernel_ms": round(kms, 4),
+                            "mrays_per_s": round(my_segs / (kms * 1e-3) / 1e6, 1),
+                            "dtype": DTYPE[pname], "parity": PARITY[pname]}
+
     result = None
     if rank == 0:
         ms_step = elapsed_s / args.steps * 1e3
@@ -227,7 +254,7 @@ def main() -> int:
             "higher_is_better": True,
             "scaling": "weak" if args.mode == "frames" else "strong",
             "vs_baseline": None,
-            "dtype": "f64" if args.precision in ("f64", "mixed") else "f32",
+            "dtype": DTYPE[args.precision],
             "data": "synthetic",
             "config": {
                 "workload": workload,
@@ -235,7 +262,7 @@ def main() -> int:
                 "width": W, "height": H, "depth": depth,
                 "spheres": n_sph, "walls": n_wall,
                 "precision": args.precision,
-                "cull_dtype": "f32" if args.precision == "mixed" else None,
+                "parity": PARITY[args.precision],
                 "frames_per_step": frames_per_step,
                 "segments_per_step": total_segs,
                 "segments_per_pixel": round(total_segs / px_step, 4),
@@ -266,6 +293,7 @@ def main() -> int:
                 "convention": "SURVEY 8d: F_seg = 30*N_sphere + 38*N_wall + 60, FMA = 2",
             },
             "cpu_baseline": None,
+            "precision_sweep": sweep or None,
         }
         if world == 1 and not args.no_cpu_baseline and args.cpu_seconds > 0:
             result["cpu_baseline"] = cpu_baseline(cfg, prims, cam, depth, flags, args.cpu_seconds)

@@ -362,3 +362,29 @@ def test_wave_cull_is_output_invariant(rend, prec):
             assert np.array_equal(imgs[0][0].view(np.uint64), imgs[1][0].view(np.uint64)), trial
     finally:
         rend.set_option(capi.RT_OPT_WAVE_CULL_MIN_SPHERES, 24)
+
+
+# ---------------------------------------------------------------- multi-GPU path (1 rank)
+def test_render_tiled_rccl_single_rank(rend):
+    """rtamd.tiling.render_tiled over the nccl (RCCL) backend with one rank: the gathered
+    frame equals a plain render (the N-rank CPU path is covered by test_dist_gloo.py)."""
+    import socket
+    import torch
+    import torch.distributed as dist
+    from rtamd import tiling
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        sc = scenes.synthetic_scene(8, 4)
+        rend.set_scene(scenes.to_prims(sc))
+        cam = capi.camera_init(**scenes.camera_args(160, 90))
+        frame = tiling.render_tiled(rend, cam, 4, capi.RT_PREC_PATH64)
+        torch.cuda.synchronize()
+        ref, _ = rend.render(cam, 4, capi.RT_PREC_PATH64, 0, capi.RT_OUT_RGB_F32)
+        assert np.array_equal(frame.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+    finally:
+        dist.destroy_process_group()
