@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""Turn a tools/make_profiles.sh run (gpurun_out/prof_<round>) into the committed
+profiles/<round>/ files and profiles/pmc_traffic.json (bench.py's roofline.traffic).
+
+HBM bytes per launch = FETCH_SIZE * 2 (gfx950 reports half of wide coalesced reads:
+MI355X_MICROARCH.md §HBM) + WRITE_SIZE, both KiB * 1024; medians over the 5 dispatches.
+"""
+import csv
+import glob
+import json
+import os
+import re
+import shutil
+import statistics
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def counters(path):
+    vals = {}
+    for r in csv.DictReader(open(path)):
+        if "k_trace" not in r["Kernel_Name"]:
+            continue
+        vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+    return {k: statistics.median(v) for k, v in vals.items()}
+
+
+def main(rnd="r01"):
+    src = os.path.join(REPO, "gpurun_out", f"prof_{rnd}")
+    dst = os.path.join(REPO, "profiles", rnd)
+    os.makedirs(dst, exist_ok=True)
+    for f in glob.glob(os.path.join(src, "bench", "**", "*.csv"), recursive=True):
+        if re.search(r"(kernel_stats|kernel_trace|agent_info)", f):
+            shutil.copy(f, os.path.join(dst, "bench_" + os.path.basename(f)))
+    bj = os.path.join(src, "bench.json")
+    if os.path.exists(bj):
+        shutil.copy(bj, os.path.join(dst, "bench_under_rocprof.json"))
+    sys.path.insert(0, os.path.join(REPO, "ray-tracer-from-scratch_amd"))
+    from rtamd import scenes
+    traffic_path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    traffic = json.load(open(traffic_path)) if os.path.exists(traffic_path) else {}
+    summary = {}
+    for d in sorted(glob.glob(os.path.join(src, "pmc_*"))):
+        if not os.path.isdir(d):
+            continue
+        _, cfg, prec, tag = os.path.basename(d).split("_", 3)
+        files = glob.glob(os.path.join(d, "**", "pmc_counter_collection.csv"), recursive=True)
+        if not files:
+            continue
+        c = counters(files[0])
+        summary.setdefault(cfg, {}).setdefault(prec, {}).update(c)
+        shutil.copy(files[0], os.path.join(dst, f"pmc_{cfg}_{prec}_{tag}.csv"))
+    for cfg, per in summary.items():
+        cf = scenes.CONFIGS[cfg]
+        sc = cf.scene()
+        n_sph = sum(1 for o in sc if o.kind == 0)
+        workload = f"{cfg}:{cf.width}x{cf.height}:d{cf.depth}:s{n_sph}w{len(sc) - n_sph}"
+        for prec, c in per.items():
+            if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+                hbm = (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024
+                traffic.setdefault(workload, {})[prec] = {
+                    "hbm_bytes_per_launch": hbm,
+                    "fetch_size_kib": c["FETCH_SIZE"], "write_size_kib": c["WRITE_SIZE"],
+                    "source": f"profiles/{rnd}/pmc_{cfg}_{prec}_*.csv",
+                }
+    json.dump(traffic, open(traffic_path, "w"), indent=1, sort_keys=True)
+    json.dump(summary, open(os.path.join(dst, "pmc_summary.json"), "w"), indent=1, sort_keys=True)
+    print(json.dumps(traffic, indent=1))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])
