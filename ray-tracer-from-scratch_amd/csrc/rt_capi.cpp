@@ -27,7 +27,7 @@ struct rt_ctx {
     bool int_exp = true;
     unsigned long long* d_stats = nullptr;
     int wave_cull_min = 24;  // spheres from which the wave cull pays (tools/sweep.py)
-    size_t off_s64 = 0, off_w32 = 0, off_w64 = 0, off_sj = 0, off_wj = 0, off_mat = 0;
+    size_t off_s64 = 0, off_w32 = 0, off_w64 = 0, off_sj = 0, off_wj = 0, off_mat = 0, off_mat32 = 0;
     void* d_out = nullptr;
     size_t d_out_cap = 0;
     unsigned long long* d_segs = nullptr;
@@ -97,6 +97,7 @@ rt::KParams make_params(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, i
     p.sph_j = reinterpret_cast<const int32_t*>(base + ctx->off_sj);
     p.wall_j = reinterpret_cast<const int32_t*>(base + ctx->off_wj);
     p.mat = reinterpret_cast<const rt::DevMat*>(base + ctx->off_mat);
+    p.mat32 = reinterpret_cast<const rt::DevMat32*>(base + ctx->off_mat32);
     p.nS = ctx->nS;
     p.nW = ctx->nW;
     p.int_exp = ctx->int_exp ? 1 : 0;
@@ -275,7 +276,8 @@ int rt_set_scene(rt_ctx* ctx, const rt_prim* prims, int32_t n) {
     const size_t off_sj = align_up(off_w64 + nW * sizeof(rt::Wall64), 256);
     const size_t off_wj = align_up(off_sj + nS * sizeof(int32_t), 256);
     const size_t off_mat = align_up(off_wj + nW * sizeof(int32_t), 256);
-    const size_t total = align_up(off_mat + (nS + nW) * sizeof(rt::DevMat), 256) + 256;
+    const size_t off_mat32 = align_up(off_mat + (nS + nW) * sizeof(rt::DevMat), 256);
+    const size_t total = align_up(off_mat32 + (nS + nW) * sizeof(rt::DevMat32), 256) + 256;
     std::vector<char> host(total, 0);
     auto* s32 = reinterpret_cast<rt::SphG32*>(host.data());
     auto* s64 = reinterpret_cast<rt::SphG64*>(host.data() + off_s64);
@@ -284,6 +286,7 @@ int rt_set_scene(rt_ctx* ctx, const rt_prim* prims, int32_t n) {
     auto* sj = reinterpret_cast<int32_t*>(host.data() + off_sj);
     auto* wj = reinterpret_cast<int32_t*>(host.data() + off_wj);
     auto* mat = reinterpret_cast<rt::DevMat*>(host.data() + off_mat);
+    auto* mat32 = reinterpret_cast<rt::DevMat32*>(host.data() + off_mat32);
     auto put_mat = [&](size_t slot, const rt_material& m) {
         rt::DevMat& d = mat[slot];
         for (int k = 0; k < 3; k++) d.color[k] = m.color[k];
@@ -292,15 +295,22 @@ int rt_set_scene(rt_ctx* ctx, const rt_prim* prims, int32_t n) {
         d.kd = m.diffuse;
         d.ks = m.specular;
         d.ex = m.specular_exponent;
+        rt::DevMat32& f = mat32[slot];
+        for (int k = 0; k < 3; k++) f.color[k] = (float)m.color[k];
+        f.ka = (float)m.ambient;
+        f.km = (float)m.metallic;
+        f.kd = (float)m.diffuse;
+        f.ks = (float)m.specular;
+        f.ex = (float)m.specular_exponent;
     };
     for (size_t s = 0; s < nS; s++) {
-        float* f = s32[s / 4].v[s % 4];
+        rt::SphG32& g = s32[s / 4];
         double* d = s64[s / 4].v[s % 4];
         for (int k = 0; k < 3; k++) {
-            f[k] = (float)sph[s].c[k];
+            g.c[k][s % 4] = (float)sph[s].c[k];
             d[k] = sph[s].c[k];
         }
-        f[3] = (float)sph[s].r;
+        g.c[3][s % 4] = (float)sph[s].r;
         d[3] = sph[s].r * sph[s].r;  // scene.cpp:51
         sj[s] = sph[s].j;
         put_mat(s, prims[sph[s].j].mat);
@@ -349,6 +359,7 @@ int rt_set_scene(rt_ctx* ctx, const rt_prim* prims, int32_t n) {
     ctx->off_sj = off_sj;
     ctx->off_wj = off_wj;
     ctx->off_mat = off_mat;
+    ctx->off_mat32 = off_mat32;
     ctx->have_scene = true;
     return RT_OK;
 }

@@ -4,13 +4,14 @@
  * HBM layout of one uploaded scene (one allocation, built by rt_set_scene; every
  * section 256-B aligned, sphere sections padded to a multiple of 4 records):
  *
- *   SphG32 [ceil(nS/4)]   4 spheres per 64 B  : {cx, cy, cz, radius}   fp32
+ *   SphG32 [ceil(nS/4)]   4 spheres per 64 B  : cx[4] cy[4] cz[4] r[4]  fp32 (SoA)
  *   SphG64 [ceil(nS/4)]   4 spheres per 128 B : {cx, cy, cz, radius^2} fp64
  *   Wall32 [nW]           64 B  : P, n, X, Y, length, width            fp32
  *   Wall64 [nW]           128 B : P, n, X, Y, length, width            fp64
  *   int32  sph_j[nS]      scene index of each sphere (tie-break only)
  *   int32  wall_j[nW]     scene index of each wall (tie-break only)
  *   DevMat [nS + nW]      64 B, spheres first then walls, indexed by "material slot"
+ *   DevMat32 [nS + nW]    32 B, fp32 copy for the fp32 colour paths
  *
  * The per-ray scan (find_closest_hit, main.cpp:67-84) runs one loop over sphere groups
  * and one over walls instead of a virtual call per primitive.  Every lane of a wave tests
@@ -31,7 +32,8 @@
 namespace rt {
 
 struct alignas(64) SphG32 {
-    float v[4][4];   // [sphere][cx, cy, cz, radius]
+    float c[4][4];   // [component cx, cy, cz, radius][sphere]: SoA so that two spheres'
+                     // same component form an SGPR pair for packed fp32 (v_pk_*) math
 };
 struct alignas(128) SphG64 {
     double v[4][4];  // [sphere][cx, cy, cz, radius*radius]
@@ -48,7 +50,12 @@ struct alignas(64) DevMat {
 };
 static_assert(sizeof(SphG32) == 64 && sizeof(SphG64) == 128, "sphere group layout");
 static_assert(sizeof(Wall32) == 64 && sizeof(Wall64) == 128, "wall layout");
+struct alignas(32) DevMat32 {
+    float color[3];
+    float ka, km, kd, ks, ex;
+};
 static_assert(sizeof(DevMat) == 64, "material layout");
+static_assert(sizeof(DevMat32) == 32, "material layout");
 
 enum { PREC_F64 = 0, PREC_F32 = 1, PREC_MIXED = 2, PREC_PATH64 = 3 };
 enum { OUT_RGB_F32 = 0, OUT_RGB_F64 = 1, OUT_RGBA8 = 2 };
@@ -67,6 +74,7 @@ struct KParams {
     const int32_t* sph_j;
     const int32_t* wall_j;
     const DevMat* mat;     // [nS + nW]
+    const DevMat32* mat32; // [nS + nW]
     int32_t nS, nW;
     int32_t int_exp;       // every specular exponent is an integer in [0, 1024]
     int32_t wave_cull;     // cull spheres per wave (rt_trace.hip) before the per-lane tests

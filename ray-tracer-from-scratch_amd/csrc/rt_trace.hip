@@ -133,6 +133,8 @@ __device__ __forceinline__ double pow_e(double x, double e) {
     return pow(x, e);
 }
 
+typedef float f2 __attribute__((ext_vector_type(2)));
+
 /* fp32 vector math (throughput path; FMAs explicit) */
 struct f3 {
     float x, y, z;
@@ -398,9 +400,9 @@ __device__ __forceinline__ uint64_t cull_chunk(const KParams& p, const Cone& cn,
     float bound = 0.0f;
     if (s < p.nS) {
         keep = true;
-        const float* S = p.s32[s >> 2].v[s & 3];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) rec.f[k] = S[k];
+        for (int k = 0; k < 4; ++k) rec.f[k] = p.s32[s >> 2].c[k][s & 3];
+        const float* S = rec.f;
         if (WANT64) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) rec.d[k] = p.s64[s >> 2].v[s & 3][k];
@@ -453,7 +455,9 @@ __device__ __forceinline__ HitD no_hit() {
 template <bool MIXED>
 __device__ __forceinline__ void sphere_by_index(const KParams& p, int s, const RayD& r,
                                                 const RayF& rf, HitD& h) {
-    if (MIXED && sphere_cull(p.s32[s >> 2].v[s & 3], rf)) return;
+    const float Sf[4] = {p.s32[s >> 2].c[0][s & 3], p.s32[s >> 2].c[1][s & 3],
+                         p.s32[s >> 2].c[2][s & 3], p.s32[s >> 2].c[3][s & 3]};
+    if (MIXED && sphere_cull(Sf, rf)) return;
     sphere_exact(p.s64[s >> 2].v[s & 3], s, r, h);
 }
 template <bool MIXED>
@@ -477,7 +481,8 @@ __device__ __forceinline__ HitD closest_hit_d(const KParams& p, const RayD& r) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const int s = 4 * g + k;
-                if (s < p.nS && !sphere_cull(G.v[k], rf)) sphere_exact(p.s64[g].v[k], s, r, h);
+                const float Sf[4] = {G.c[0][k], G.c[1][k], G.c[2][k], G.c[3][k]};
+                if (s < p.nS && !sphere_cull(Sf, rf)) sphere_exact(p.s64[g].v[k], s, r, h);
             }
         } else {
             const SphG64 G = p.s64[g];  // two s_load_dwordx16
@@ -550,9 +555,9 @@ __device__ __forceinline__ RayD make_ray(d3 o, d3 d) {
 
 /* fp32 shading of one hit for PATH64: the same formulas as shade_d on the exact fp64
  * geometry rounded to fp32 (colour only — nothing here feeds the next ray). */
-__device__ __forceinline__ float2 shade_f(const DevMat& m, const f3 pos, const f3 nn,
+__device__ __forceinline__ float2 shade_f(const DevMat32& m, const f3 pos, const f3 nn,
                                           const f3 nv, bool sun) {
-    const float kd = (float)m.kd, ks = (float)m.ks, ka = (float)m.ka, ex = (float)m.ex;
+    const float kd = m.kd, ks = m.ks, ka = m.ka, ex = m.ex;
     const f3 ldir = fnormalize(-pos);
     const float lamb = fmaxf(fdot(ldir, nn), 0.0f);
     const float res = fmaxf(fdot(fnormalize(ldir - nv), nn), 0.0f);
@@ -567,8 +572,8 @@ __device__ __forceinline__ float2 shade_f(const DevMat& m, const f3 pos, const f
     }
     return r;
 }
-__device__ __forceinline__ f3 local_color_f(const DevMat& m, float s, float ksun, bool sun) {
-    const f3 col = F3((float)m.color[0], (float)m.color[1], (float)m.color[2]);
+__device__ __forceinline__ f3 local_color_f(const DevMat32& m, float s, float ksun, bool sun) {
+    const f3 col = F3(m.color[0], m.color[1], m.color[2]);
     f3 L = col * s;
     if (sun) L = fmad3(F3(1.64f * col.x, 1.27f * col.y, 0.99f * col.z), ksun, L);
     return L;
@@ -664,7 +669,7 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
             s = sh.s;
             ks = sh.ksun;
         } else {
-            const float2 sh = shade_f(m, tof(pos), tof(nn), tof(nv), sun);
+            const float2 sh = shade_f(p.mat32[h.slot], tof(pos), tof(nn), tof(nv), sun);
             s = sh.x;
             ks = sh.y;
         }
@@ -672,7 +677,7 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
             if (COLOR64)
                 c64 = local_color_d(m, s, ks, sun);
             else
-                c32 = local_color_f(m, s, ks, sun);
+                c32 = local_color_f(p.mat32[h.slot], s, ks, sun);
             alive = false;
             continue;
         }
@@ -691,8 +696,9 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
                 const d3 L = local_color_d(m, st_s[q], st_k[q], sun);
                 c64 = lerp(L, c64, m.km);  // vec.cpp:45-49 via main.cpp:117
             } else {
-                const f3 L = local_color_f(m, st_s[q], st_k[q], sun);
-                const float km = (float)m.km;
+                const DevMat32& m32 = p.mat32[st_m[q]];
+                const f3 L = local_color_f(m32, st_s[q], st_k[q], sun);
+                const float km = m32.km;
                 c32 = F3(fmaf(km, c32.x - L.x, L.x), fmaf(km, c32.y - L.y, L.y),
                          fmaf(km, c32.z - L.z, L.z));
             }
@@ -727,6 +733,37 @@ __device__ __forceinline__ void sphere_f(const float* S, int s, f3 o, f3 d, floa
             best = dist;
             bpt = (det == 0.0f) ? -bh * ra : proj;
             slot = s;
+        }
+    }
+}
+
+/* Two spheres (k0, k0+1 of group G) per packed fp32 instruction: the cheap prefix
+ * (oc, b/2, c, det) runs as v_pk_* on {sphere k0, sphere k0+1}; the rare hit path
+ * (sqrt, divide, compare) per sphere.  Same arithmetic as sphere_f, lane for lane. */
+__device__ __forceinline__ void sphere_pair_f(const SphG32& G, int k0, int s0, int nS, f3 o,
+                                              f3 d, float a, float ra, float rl, float& best,
+                                              float& bpt, int& slot) {
+    const f2 cx = {G.c[0][k0], G.c[0][k0 + 1]}, cy = {G.c[1][k0], G.c[1][k0 + 1]};
+    const f2 cz = {G.c[2][k0], G.c[2][k0 + 1]}, rr = {G.c[3][k0], G.c[3][k0 + 1]};
+    const f2 ocx = f2(o.x) - cx, ocy = f2(o.y) - cy, ocz = f2(o.z) - cz;
+    const f2 bh = __builtin_elementwise_fma(
+        f2(d.x), ocx, __builtin_elementwise_fma(f2(d.y), ocy, f2(d.z) * ocz));
+    const f2 cq = __builtin_elementwise_fma(
+        -rr, rr, __builtin_elementwise_fma(ocx, ocx, __builtin_elementwise_fma(ocy, ocy, ocz * ocz)));
+    const f2 det = __builtin_elementwise_fma(bh, bh, -f2(a) * cq);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        if (s0 + k >= nS) break;
+        const float b1 = bh[k], d1 = det[k];
+        if (b1 <= 0.0f && d1 >= 0.0f) {
+            const float num = -b1 - fsqrt(d1);
+            const float proj = (d1 == 0.0f) ? -2.0f * b1 * ra : num * ra;
+            const float dist = proj * a * rl;
+            if ((d1 == 0.0f || num > 0.0f) && dist > 0.0f && dist < best) {
+                best = dist;
+                bpt = (d1 == 0.0f) ? -b1 * ra : proj;
+                slot = s0 + k;
+            }
         }
     }
 }
@@ -796,12 +833,12 @@ __device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, bool
         } else if (alive) {
             const int ng = (p.nS + 3) >> 2;
             for (int g = 0; g < ng; ++g) {
-                const SphG32 G = p.s32[g];
+                const SphG32 G = p.s32[g];  // one s_load_dwordx16
 #pragma unroll
-                for (int kk = 0; kk < 4; ++kk) {
-                    const int sidx = 4 * g + kk;
-                    if (sidx >= p.nS) break;
-                    sphere_f(G.v[kk], sidx, o, d, a, ra, rl, best, bpt, slot);
+                for (int h2 = 0; h2 < 2; ++h2) {
+                    const int s0 = 4 * g + 2 * h2;
+                    if (s0 >= p.nS) break;
+                    sphere_pair_f(G, 2 * h2, s0, p.nS, o, d, a, ra, rl, best, bpt, slot);
                 }
             }
         }
@@ -823,13 +860,13 @@ __device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, bool
         const f3 pos = fmad3(d, best, o);
         f3 N;
         if (slot < p.nS) {
-            const float* S = p.s32[slot >> 2].v[slot & 3];
-            N = fmad3(d, bpt, o) - F3(S[0], S[1], S[2]);
+            const SphG32& G = p.s32[slot >> 2];
+            N = fmad3(d, bpt, o) - F3(G.c[0][slot & 3], G.c[1][slot & 3], G.c[2][slot & 3]);
         } else {
             const Wall32& Wl = p.w32[slot - p.nS];
             N = F3(Wl.n[0], Wl.n[1], Wl.n[2]);
         }
-        const DevMat& m = p.mat[slot];
+        const DevMat32& m = p.mat32[slot];
         const f3 nn = fnormalize(N);
         const float2 sh = shade_f(m, pos, nn, nv, sun);
         if (k >= p.depth || k >= MAXD) {
@@ -847,9 +884,9 @@ __device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, bool
     }
     for (int q = MAXD - 1; q >= 0; --q) {
         if (q < n) {
-            const DevMat& m = p.mat[st_m[q]];
+            const DevMat32& m = p.mat32[st_m[q]];
             const f3 L = local_color_f(m, st_s[q], st_k[q], sun);
-            const float km = (float)m.km;
+            const float km = m.km;
             c = F3(fmaf(km, c.x - L.x, L.x), fmaf(km, c.y - L.y, L.y), fmaf(km, c.z - L.z, L.z));
         }
     }
