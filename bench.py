@@ -154,23 +154,24 @@ def main() -> int:
     torch.cuda.set_stream(stream)
     out = torch.empty((band_max, W, 3), dtype=torch.float32, device=dev)
     segs_t = torch.zeros(1, dtype=torch.int64, device=dev)
-    frame = torch.empty((H, W, 3), dtype=torch.float32, device=dev) if (
-        args.mode == "tiled" and rank == 0) else None
-    gather_list = ([torch.empty_like(out) for _ in range(world)]
-                   if (args.mode == "tiled" and rank == 0 and world > 1) else None)
 
-    def launch(d_segs: int = 0):
-        rend.render_device(cam, depth, out.data_ptr(), prec, flags, capi.RT_OUT_RGB_F32,
-                           row0=row0, nrows=nrows, d_segments=d_segs, stream=stream.cuda_stream)
+    def launch(d_segs: int = 0, dst=None):
+        rend.render_device(cam, depth, (dst if dst is not None else out).data_ptr(), prec, flags,
+                           capi.RT_OUT_RGB_F32, row0=row0, nrows=nrows, d_segments=d_segs,
+                           stream=stream.cuda_stream)
+
+    tiled = None
+    if args.mode == "tiled" and world > 1:
+        from rtamd import tiling
+        # double-buffered: the gather of frame k (RCCL stream) overlaps the render of k+1
+        tiled = tiling.TiledFrames(lambda r0, n, buf: launch(dst=buf), H, W, 3, torch.float32,
+                                   dev, depth=2)
 
     def step():
-        launch()
-        if args.mode == "tiled" and world > 1:
-            dist.gather(out, gather_list, dst=0)
-            if rank == 0:
-                for r, g in enumerate(gather_list):
-                    a, n = capi.band_rows(H, world, r)
-                    frame[a:a + n].copy_(g[:n])
+        if tiled is not None:
+            tiled.submit()
+        else:
+            launch()
 
     # census: exact segment count of this rank's share (untimed)
     launch(segs_t.data_ptr())
@@ -183,6 +184,8 @@ def main() -> int:
 
     for _ in range(args.warmup):
         step()
+    if tiled is not None:
+        tiled.drain()
     barrier()
     torch.cuda.synchronize(dev)
     ev0 = torch.cuda.Event(enable_timing=True)
@@ -191,6 +194,8 @@ def main() -> int:
     ev0.record(stream)
     for _ in range(args.steps):
         step()
+    if tiled is not None:
+        tiled.drain()
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     barrier()

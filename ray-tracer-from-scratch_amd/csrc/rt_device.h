@@ -61,10 +61,15 @@ enum { PREC_F64 = 0, PREC_F32 = 1, PREC_MIXED = 2, PREC_PATH64 = 3 };
 enum { OUT_RGB_F32 = 0, OUT_RGB_F64 = 1, OUT_RGBA8 = 2 };
 enum { FLAG_SUN = 1 };
 
-// Pixel tile of one 256-thread workgroup: 4 waves, each an 8x8 pixel square.
-constexpr int TILE_W = 16;
-constexpr int TILE_H = 16;
-constexpr int BLOCK = 256;
+// Pixel tile of one workgroup: RT_WAVES_PER_BLOCK waves (1, 2 or 4), each an 8x8 square.
+// One wave per workgroup measured fastest (tools/ab.py: c5 -15..21%, c3 -7..12%, c2 -2%
+// vs four): finer dispatch granularity at 3-5 waves/SIMD.
+#ifndef RT_WAVES_PER_BLOCK
+#define RT_WAVES_PER_BLOCK 1
+#endif
+constexpr int BLOCK = 64 * RT_WAVES_PER_BLOCK;
+constexpr int TILE_W = RT_WAVES_PER_BLOCK >= 2 ? 16 : 8;
+constexpr int TILE_H = RT_WAVES_PER_BLOCK >= 4 ? 16 : 8;
 
 struct KParams {
     const SphG32* s32;

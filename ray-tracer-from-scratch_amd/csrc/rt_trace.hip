@@ -938,7 +938,7 @@ constexpr int waves_per_eu() {
     // (ScratchSize 0 for every no-sun integer-exponent variant; the rare sun +
     // non-integer-exponent deep fp64 variants run at 2 waves and may spill a little).
     const int tier = MAXD >= 16 ? 2 : (MAXD >= 10 ? 1 : 0);
-    int w;
+    int w = 0;
     if (PREC == PREC_F32)
         w = 5 - (tier > 0 ? 1 : 0) - ((SUN && tier == 2) ? 1 : 0);
     else if (PREC == PREC_PATH64)
@@ -955,8 +955,8 @@ __attribute__((amdgpu_waves_per_eu(waves_per_eu<PREC, SUN, INT_EXP, CULL, MAXD>(
 k_trace(KParams p) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    const int x = blockIdx.x * TILE_W + (wave & 1) * 8 + (lane & 7);
-    const int r = blockIdx.y * TILE_H + (wave >> 1) * 8 + (lane >> 3);
+    const int x = blockIdx.x * TILE_W + (TILE_W > 8 ? (wave & 1) * 8 : 0) + (lane & 7);
+    const int r = blockIdx.y * TILE_H + (TILE_H > 8 ? (wave >> 1) * 8 : 0) + (lane >> 3);
     const bool valid = x < p.W && r < p.nrows;
     const int i = p.row0 + r;
     int segs = 0;

@@ -41,11 +41,32 @@ def _worker(rank, world, port, w, h, depth, q):
         frame = tiling.gather_frame(band, h, w, 3, torch.float64, torch.device("cpu"))
         if rank == 0:
             q.put(frame.numpy().copy())
+        # frames back to back with double buffering: frame k = camera moved k steps
+        shift = {"k": 0}
+
+        def band_k(row0, nrows, out):
+            c2 = orc.camera_init(**scenes.camera_args(w, h))
+            c2.position[0] += 0.1 * shift["k"]
+            o64, _, _ = orc.render(prims, c2, depth, row0=row0, nrows=nrows, nthreads=1)
+            out[:nrows] = torch.from_numpy(o64)
+
+        tf = tiling.TiledFrames(band_k, h, w, 3, torch.float64, torch.device("cpu"), depth=2)
+        for k in range(3):
+            shift["k"] = k
+            hd = tf.submit()
+            if k >= 1:       # frame k-1 completes while frame k was submitted
+                prev = (hd[0] + 1) % 2
+                tf.wait(tf.pending[prev]) if tf.pending[prev] is not None else None
+                if rank == 0:
+                    q.put(("seq", k - 1, tf.frame(prev).numpy().copy()))
+        tf.drain()
+        if rank == 0:
+            q.put(("seq", 2, tf.frame(2 % 2).numpy().copy()))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,w,h", [(2, 48, 27), (3, 40, 37)])
+@pytest.mark.parametrize("world,w,h", [(2, 48, 27), (3, 40, 37), (2, 32, 20)])
 def test_row_tiled_gather_equals_single_frame(world, w, h, oracle):
     from rtamd import scenes
     ctx = mp.get_context("spawn")
@@ -55,12 +76,19 @@ def test_row_tiled_gather_equals_single_frame(world, w, h, oracle):
     for p in procs:
         p.start()
     frame = q.get(timeout=120)
+    seq = [q.get(timeout=120) for _ in range(3)]
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
+    prims = scenes.to_prims(scenes.synthetic_scene(8, 4))
     cam = oracle.camera_init(**scenes.camera_args(w, h))
-    ref, _, _ = oracle.render(scenes.to_prims(scenes.synthetic_scene(8, 4)), cam, 4)
+    ref, _, _ = oracle.render(prims, cam, 4)
     assert np.array_equal(frame.view(np.uint64), ref.view(np.uint64))
+    for tag, k, img in seq:
+        c2 = oracle.camera_init(**scenes.camera_args(w, h))
+        c2.position[0] += 0.1 * k
+        r2, _, _ = oracle.render(prims, c2, 4)
+        assert np.array_equal(img.view(np.uint64), r2.view(np.uint64)), k
 
 
 def test_band_partition_matches_c_abi():
