@@ -50,6 +50,9 @@
 #ifndef RT_WALLS_FIRST
 #define RT_WALLS_FIRST 1
 #endif
+#ifndef RT_F32_READLANE   // F32 survivor records: 1 = v_readlane from the culling lane,
+#define RT_F32_READLANE 0 // 0 = scalar loads (A/B: c5 -13%); fp64 paths keep v_readlane
+#endif
 
 namespace rt {
 
@@ -823,9 +826,21 @@ __device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, bool
                     while (m) {
                         const int l = __builtin_ctzll(m);
                         m &= m - 1;
-                        const float Sf[4] = {lane_f(rec.f[0], l), lane_f(rec.f[1], l),
-                                             lane_f(rec.f[2], l), lane_f(rec.f[3], l)};
-                        sphere_f<false>(Sf, c0 + l, o, d, a, ra, rl, best, bpt, slot, &p);
+                        const int sidx = c0 + l;
+                        float Sf[4];
+                        if (RT_F32_READLANE) {
+                            Sf[0] = lane_f(rec.f[0], l);
+                            Sf[1] = lane_f(rec.f[1], l);
+                            Sf[2] = lane_f(rec.f[2], l);
+                            Sf[3] = lane_f(rec.f[3], l);
+                        } else {
+                            const SphG32& G = p.s32[sidx >> 2];
+                            Sf[0] = G.c[0][sidx & 3];
+                            Sf[1] = G.c[1][sidx & 3];
+                            Sf[2] = G.c[2][sidx & 3];
+                            Sf[3] = G.c[3][sidx & 3];
+                        }
+                        sphere_f<false>(Sf, sidx, o, d, a, ra, rl, best, bpt, slot, &p);
                     }
                 }
             }
@@ -945,7 +960,7 @@ constexpr int waves_per_eu() {
         w = 4 - (tier == 2 ? 1 : 0) - ((SUN && tier > 0) ? 1 : 0);
     else
         w = (INT_EXP ? (SUN ? 3 : 4) : (SUN ? 2 : 3)) - (tier > 0 ? 1 : 0) -
-            ((CULL && MAXD >= 8) ? 1 : 0);
+            ((PREC == PREC_MIXED && CULL && MAXD >= 8) ? 1 : 0);  // A/B: F64 faster at 4
     return w < 2 ? 2 : w;
 }
 
