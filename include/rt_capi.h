@@ -135,9 +135,12 @@ enum rt_option {
     RT_OPT_WAVE_CULL_MIN_SPHERES = 1, /* scenes with at least this many spheres use the
                                          wave-cooperative cull (default 24; 0 = always,
                                          INT32_MAX = never).  Output is identical. */
-    RT_OPT_STATS_DEVICE_PTR = 2       /* diagnostics: device address of 3 uint64 counters
+    RT_OPT_STATS_DEVICE_PTR = 2,      /* diagnostics: device address of 3 uint64 counters
                                          that renders add to ([0] wave culls, [1] spheres
                                          kept, [2] spheres considered); 0 = off */
+    RT_OPT_EYE_TABLES = 3             /* 1 (default): primary rays use per-frame tables of
+                                         their camera-origin terms (small scenes); 0 = off.
+                                         Output is identical. */
 };
 int rt_set_option(rt_ctx* ctx, int32_t option, int64_t value);
 

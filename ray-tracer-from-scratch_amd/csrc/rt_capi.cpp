@@ -27,10 +27,13 @@ struct rt_ctx {
     bool int_exp = true;
     unsigned long long* d_stats = nullptr;
     int wave_cull_min = 24;  // spheres from which the wave cull pays (tools/sweep.py)
+    bool eye_tables = true;  // RT_OPT_EYE_TABLES
     size_t off_s64 = 0, off_w32 = 0, off_w64 = 0, off_sj = 0, off_wj = 0, off_mat = 0, off_mat32 = 0;
     void* d_out = nullptr;
     size_t d_out_cap = 0;
     unsigned long long* d_segs = nullptr;
+    std::vector<double> h_sph;  // host copy: nS x {cx, cy, cz, radius^2}
+    std::vector<double> h_wal;  // host copy: nW x {P, n}
     char last_err[256] = {0};
 };
 
@@ -117,6 +120,24 @@ rt::KParams make_params(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, i
     p.out = d_out;
     p.segs = d_segs;
     p.stats = ctx->d_stats;
+    // eye tables (rt_device.h) for the linear-scan kernels: the same fp64 operations, in
+    // the same order, as sphere_exact / wall_exact on a ray starting at cam->position
+    p.eye = (ctx->eye_tables && !p.wave_cull && ctx->nS <= rt::EYE_MAX_S && ctx->nW <= rt::EYE_MAX_W) ? 1 : 0;
+    if (p.eye) {
+        const double* o = cam->position;
+        for (int s = 0; s < ctx->nS; s++) {
+            const double* S = &ctx->h_sph[4 * s];
+            const double ox = o[0] - S[0], oy = o[1] - S[1], oz = o[2] - S[2];  // scene.cpp:45
+            const double c = (ox * ox + oy * oy + oz * oz) - S[3];              // scene.cpp:51
+            const double e[4] = {ox, oy, oz, c};
+            for (int k = 0; k < 4; k++) p.eye_s[s][k] = e[k];
+        }
+        for (int w = 0; w < ctx->nW; w++) {
+            const double* P = &ctx->h_wal[6 * w];
+            const double* n = P + 3;
+            p.eye_w[w] = (P[0] - o[0]) * n[0] + (P[1] - o[1]) * n[1] + (P[2] - o[2]) * n[2];  // scene.cpp:10
+        }
+    }
     return p;
 }
 
@@ -353,6 +374,15 @@ int rt_set_scene(rt_ctx* ctx, const rt_prim* prims, int32_t n) {
         const double e = mat[k].ex;
         if (!(e >= 0.0 && e <= 1024.0 && e == std::floor(e))) ctx->int_exp = false;
     }
+    ctx->h_sph.assign(4 * nS, 0.0);
+    for (size_t s = 0; s < nS; s++)
+        for (int k = 0; k < 4; k++) ctx->h_sph[4 * s + k] = s64[s / 4].v[s % 4][k];
+    ctx->h_wal.assign(6 * nW, 0.0);
+    for (size_t w = 0; w < nW; w++)
+        for (int k = 0; k < 3; k++) {
+            ctx->h_wal[6 * w + k] = w64[w].P[k];
+            ctx->h_wal[6 * w + 3 + k] = w64[w].n[k];
+        }
     ctx->off_s64 = off_s64;
     ctx->off_w32 = off_w32;
     ctx->off_w64 = off_w64;
@@ -373,6 +403,10 @@ int rt_set_option(rt_ctx* ctx, int32_t option, int64_t value) {
             return RT_OK;
         case RT_OPT_STATS_DEVICE_PTR:
             ctx->d_stats = reinterpret_cast<unsigned long long*>(static_cast<intptr_t>(value));
+            return RT_OK;
+        case RT_OPT_EYE_TABLES:
+            if (value != 0 && value != 1) return RT_ERR_INVALID_ARG;
+            ctx->eye_tables = value == 1;
             return RT_OK;
         default:
             return RT_ERR_INVALID_ARG;

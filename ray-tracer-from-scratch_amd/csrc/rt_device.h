@@ -71,6 +71,18 @@ constexpr int BLOCK = 64 * RT_WAVES_PER_BLOCK;
 constexpr int TILE_W = RT_WAVES_PER_BLOCK >= 2 ? 16 : 8;
 constexpr int TILE_H = RT_WAVES_PER_BLOCK >= 4 ? 16 : 8;
 
+// Camera-origin ("eye") tables of the primary segment.  Every primary ray starts at the
+// camera position, so the origin-only terms of both tests — Sphere::intersect's
+// ray_sphere_vec and c (scene.cpp:45, 51) and Wall::intersect's numerator
+// dot(position - origin, normal) (scene.cpp:10) — are the same for every pixel of a
+// frame.  The host evaluates them once per render with the reference's fp64 operations
+// (bit-identical values) and passes them in the kernel arguments, which the kernel reads
+// with scalar loads: the primary test then costs the direction-dependent half only.
+// Used by the F64/PATH64 linear-scan kernels when the scene fits (eye != 0); A/B at
+// c2: -2..3%.  (The fp32 path measured slower with them.)
+constexpr int EYE_MAX_S = 32;
+constexpr int EYE_MAX_W = 16;
+
 struct KParams {
     const SphG32* s32;
     const SphG64* s64;
@@ -90,6 +102,10 @@ struct KParams {
     void* out;
     unsigned long long* segs;   // may be null
     unsigned long long* stats;  // diagnostic counters, may be null (rt_set_option)
+    int32_t eye;                        // eye tables below valid
+    int32_t pad_eye;
+    double eye_s[EYE_MAX_S][4];         // sphere s: {oc.x, oc.y, oc.z, |oc|^2 - r^2}
+    double eye_w[EYE_MAX_W];            // wall w: dot(P - pos, n)
 };
 
 // Host-side launchers (rt_trace.hip).  Return a hipError_t as int.

@@ -50,6 +50,12 @@
 #ifndef RT_WALLS_FIRST
 #define RT_WALLS_FIRST 1
 #endif
+#ifndef RT_WALL_TSKIP      // 1: a wall whose t exceeds the current best skips its bounds
+#define RT_WALL_TSKIP 1    // test (exact: the reference's strict < rejects it anyway);
+#endif                     // fp64 paths only (the branch costs the fp32 path ~1% at c5)
+#ifndef RT_TERMINAL_F32    // PATH64: the last segment of a path (sky, or the hit at max
+#define RT_TERMINAL_F32 1  // depth) feeds colour only, so its normalisations run in fp32
+#endif
 #ifndef RT_F32_READLANE   // F32 survivor records: 1 = v_readlane from the culling lane,
 #define RT_F32_READLANE 0 // 0 = scalar loads (A/B: c5 -13%); fp64 paths keep v_readlane
 #endif
@@ -209,13 +215,13 @@ __device__ __forceinline__ int scene_index(const KParams& p, int slot) {
 
 /* IN_ORDER: spheres visited in increasing index before any wall, so a tie keeps the
  * earlier hit (strict <, main.cpp:77); otherwise a tie compares scene indices. */
+/* oc = origin - center and c = |oc|^2 - r^2 given (eye tables) or computed here. */
 template <bool IN_ORDER = true>
-__device__ __forceinline__ void sphere_exact(const double* S, int s, const RayD& r, HitD& h,
-                                             const KParams* p = nullptr) {
-    const d3 oc = r.o - D3(S[0], S[1], S[2]);
+__device__ __forceinline__ void sphere_exact_oc(const d3 oc, const double c, int s,
+                                                const RayD& r, HitD& h,
+                                                const KParams* p = nullptr) {
     const double dt = dot(r.d, oc);  // b / 2
     if (dt > 0) return;
-    const double c = lensq(oc) - S[3];
     const double x = dt * dt - r.a * c;  // det / 4
     if (!(x >= 0)) return;
     double proj, pt;
@@ -238,18 +244,26 @@ __device__ __forceinline__ void sphere_exact(const double* S, int s, const RayD&
         h.slot = s;
     }
 }
+template <bool IN_ORDER = true>
+__device__ __forceinline__ void sphere_exact(const double* S, int s, const RayD& r, HitD& h,
+                                             const KParams* p = nullptr) {
+    const d3 oc = r.o - D3(S[0], S[1], S[2]);
+    sphere_exact_oc<IN_ORDER>(oc, lensq(oc) - S[3], s, r, h, p);
+}
 
 /* Wall::intersect (scene.cpp:4-35), exact.  t = num/denom is formed only when the signs
  * make t > 0 possible (denom == 0 or NaN can never pass the bounds check). */
+template <bool EYE = false>
 __device__ __forceinline__ void wall_exact(const Wall64& Wl, int w, const KParams& p,
                                            const RayD& r, HitD& h) {
     const d3 n = ld3(Wl.n);
     const d3 P = ld3(Wl.P);
     const double den = dot(n, r.d);
-    const double num = dot(P - r.o, n);
+    const double num = EYE ? p.eye_w[w] : dot(P - r.o, n);
     if (!((num > 0 && den > 0) || (num < 0 && den < 0))) return;
     const double t = div_r(num, den, rcp_refined(den));
     if (!(t > 0)) return;
+    if (RT_WALL_TSKIP && t > h.dist) return;  // loses to the current best either way
     const d3 q = (r.o + r.d * t) - P;  // ray::at (scene.h:16) minus the corner
     const double px = dot(q, ld3(Wl.X));
     const double py = dot(q, ld3(Wl.Y));
@@ -463,16 +477,17 @@ __device__ __forceinline__ void sphere_by_index(const KParams& p, int s, const R
     if (MIXED && sphere_cull(Sf, rf)) return;
     sphere_exact(p.s64[s >> 2].v[s & 3], s, r, h);
 }
-template <bool MIXED>
+template <bool MIXED, bool EYE = false>
 __device__ __forceinline__ void walls_d(const KParams& p, const RayD& r, const RayF& rf, HitD& h) {
     for (int w = 0; w < p.nW; ++w) {
         if (MIXED && wall_cull(p.w32[w], rf)) continue;
-        wall_exact(p.w64[w], w, p, r, h);
+        wall_exact<EYE>(p.w64[w], w, p, r, h);
     }
 }
 
-/* Linear scan (no wave cull): groups of 4 spheres per scalar load. */
-template <bool MIXED>
+/* Linear scan (no wave cull): groups of 4 spheres per scalar load.  EYE: the primary
+ * segment, origin terms from the eye tables (rt_device.h). */
+template <bool MIXED, bool EYE>
 __device__ __forceinline__ HitD closest_hit_d(const KParams& p, const RayD& r) {
     HitD h = no_hit();
     RayF rf;
@@ -485,7 +500,21 @@ __device__ __forceinline__ HitD closest_hit_d(const KParams& p, const RayD& r) {
             for (int k = 0; k < 4; ++k) {
                 const int s = 4 * g + k;
                 const float Sf[4] = {G.c[0][k], G.c[1][k], G.c[2][k], G.c[3][k]};
-                if (s < p.nS && !sphere_cull(Sf, rf)) sphere_exact(p.s64[g].v[k], s, r, h);
+                if (s < p.nS && !sphere_cull(Sf, rf)) {
+                    if (EYE) {
+                        const double* E = p.eye_s[s];
+                        sphere_exact_oc(D3(E[0], E[1], E[2]), E[3], s, r, h);
+                    } else {
+                        sphere_exact(p.s64[g].v[k], s, r, h);
+                    }
+                }
+            }
+        } else if (EYE) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int s = 4 * g + k;
+                const double* E = p.eye_s[s];
+                if (s < p.nS) sphere_exact_oc(D3(E[0], E[1], E[2]), E[3], s, r, h);
             }
         } else {
             const SphG64 G = p.s64[g];  // two s_load_dwordx16
@@ -496,7 +525,7 @@ __device__ __forceinline__ HitD closest_hit_d(const KParams& p, const RayD& r) {
             }
         }
     }
-    walls_d<MIXED>(p, r, rf, h);
+    walls_d<MIXED, EYE>(p, r, rf, h);
     return h;
 }
 
@@ -637,10 +666,42 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
             }
             if (!RT_WALLS_FIRST && alive) walls_d<MIXED>(p, r, rf, h);
         } else if (alive) {
-            h = closest_hit_d<MIXED>(p, r);
+            // k == 0 and p.eye are wave-uniform: one scan or the other per wave (MIXED
+            // keeps its fp32 cull in front of every test: no eye tables, A/B +1.5%)
+            h = (!MIXED && k == 0 && p.eye) ? closest_hit_d<MIXED, true>(p, r)
+                                  : closest_hit_d<MIXED, false>(p, r);
         }
         if (!alive) continue;
         ++segs;
+        const bool last = k >= p.depth || k >= MAXD;  // remaining_iterations <= 0 (main.cpp:105)
+        if (!COLOR64 && RT_TERMINAL_F32 && (last || h.slot < 0)) {
+            // PATH64, last segment of the path: nothing here feeds another ray
+            const f3 d32 = tof(r.d);
+            const f3 nv32 = fnormalize(d32);
+            if (h.slot < 0) {
+                if (r.d.z < 0.0) {
+                    c32 = F3(0.025f, 0.05f, 0.075f);
+                } else {
+                    const float tz = fsqrt(fsqrt(nv32.z));
+                    c32 = F3(fmaf(tz, 0.14f - 0.36f, 0.36f), fmaf(tz, 0.21f - 0.45f, 0.45f),
+                             fmaf(tz, 0.49f - 0.57f, 0.57f));
+                }
+            } else {
+                const d3 pos = r.o + r.d * h.dist;
+                f3 N32;
+                if (h.slot < p.nS) {
+                    const double* S = p.s64[h.slot >> 2].v[h.slot & 3];
+                    N32 = tof((r.o + r.d * h.pt) - D3(S[0], S[1], S[2]));
+                } else {
+                    N32 = tof(ld3(p.w64[h.slot - p.nS].n));
+                }
+                const DevMat32& m32 = p.mat32[h.slot];
+                const float2 sh = shade_f(m32, tof(pos), fnormalize(N32), nv32, sun);
+                c32 = local_color_f(m32, sh.x, sh.y, sun);
+            }
+            alive = false;
+            continue;
+        }
         const double rdl = rcp_refined(r.dlen);
         const d3 nv = div3(r.d, r.dlen, rdl);  // normalize(d); normalize(-d) == -nv
         if (h.slot < 0) {
@@ -676,7 +737,7 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
             s = sh.x;
             ks = sh.y;
         }
-        if (k >= p.depth || k >= MAXD) {  // remaining_iterations <= 0 (main.cpp:105)
+        if (last) {
             if (COLOR64)
                 c64 = local_color_d(m, s, ks, sun);
             else

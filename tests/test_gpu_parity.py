@@ -364,6 +364,37 @@ def test_wave_cull_is_output_invariant(rend, prec):
         rend.set_option(capi.RT_OPT_WAVE_CULL_MIN_SPHERES, 24)
 
 
+# ---------------------------------------------------------------- eye tables
+@pytest.mark.parametrize("prec", [capi.RT_PREC_F64, capi.RT_PREC_MIXED, capi.RT_PREC_PATH64])
+def test_eye_tables_are_output_invariant(rend, prec):
+    """Primary rays read their camera-origin terms from host-computed tables (rt_device.h
+    "eye tables"): for the exact precisions frames with and without them are bitwise
+    identical, up to the table limits (32 spheres, 16 walls) and past them (off)."""
+    rng = np.random.default_rng(12)
+    try:
+        for trial, (ns, nw) in enumerate(((1, 0), (5, 3), (8, 4), (23, 7), (32, 16), (33, 2))):
+            sc = scenes.synthetic_scene(ns, min(nw, 6), seed=int(rng.integers(1 << 30)))
+            for _ in range(nw - 6):  # random extra walls
+                nrm = rng.normal(size=3)
+                sc.append(scenes.Wall(scenes.Material(tuple(rng.uniform(0, 1, 3)), .5),
+                                      tuple(rng.uniform(-6, 6, 3)), tuple(nrm / np.linalg.norm(nrm)),
+                                      float(rng.uniform(1, 8)), float(rng.uniform(1, 8))))
+            rend.set_scene(scenes.to_prims(sc))
+            pos = rng.uniform([-1, -3, -1], [5, 3, 2])
+            cam = capi.camera_init(pos, pos + rng.normal(size=3), (0, 0, -1),
+                                   float(rng.uniform(40, 110)), 16 / 9, 160.0)
+            depth = int(rng.integers(1, 7))
+            imgs = []
+            for eye in (1, 0):
+                rend.set_option(capi.RT_OPT_EYE_TABLES, eye)
+                img, st = rend.render(cam, depth, prec, 0, capi.RT_OUT_RGB_F64, count_segments=True)
+                imgs.append((img, st.segments))
+            assert imgs[0][1] == imgs[1][1], trial
+            assert np.array_equal(imgs[0][0].view(np.uint64), imgs[1][0].view(np.uint64)), trial
+    finally:
+        rend.set_option(capi.RT_OPT_EYE_TABLES, 1)
+
+
 # ---------------------------------------------------------------- multi-GPU path (1 rank)
 def test_render_tiled_rccl_single_rank(rend):
     """rtamd.tiling.render_tiled over the nccl (RCCL) backend with one rank: the gathered

@@ -1,0 +1,13 @@
+#!/usr/bin/env bash
+# Build librt_amd.so with extra compile definitions into ray-tracer-from-scratch_amd/lib/ab/
+# for in-process A/B (tools/ab.py).   Usage: tools/build_variant.sh NAME [-DX=1 ...]
+set -eu
+cd "$(dirname "$0")/../ray-tracer-from-scratch_amd"
+name=$1; shift
+B=build/ab_$name; mkdir -p "$B" lib/ab
+F="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off -munsafe-fp-atomics -I../include"
+/opt/rocm/bin/hipcc $F "$@" -c csrc/rt_trace.hip -o "$B/rt_trace.o" &
+/opt/rocm/bin/hipcc $F "$@" -x hip -c csrc/rt_capi.cpp -o "$B/rt_capi.o" &
+wait
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o "lib/ab/$name.so" "$B/rt_trace.o" "$B/rt_capi.o"
+echo "lib/ab/$name.so"

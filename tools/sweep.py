@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--sun", action="store_true")
     ap.add_argument("--cull", default="default", help="wave-cull min spheres: default|always|never|N")
+    ap.add_argument("--depths", default="", help="comma-separated depths overriding the config's")
+    ap.add_argument("--eye", type=int, default=1, help="RT_OPT_EYE_TABLES (0/1)")
     args = ap.parse_args()
     import torch
     dev = torch.device("cuda", 0)
@@ -33,10 +35,15 @@ def main():
         cull = int(args.cull)
     if cull is not None:
         rend.set_option(capi.RT_OPT_WAVE_CULL_MIN_SPHERES, cull)
+    rend.set_option(capi.RT_OPT_EYE_TABLES, args.eye)
     flags = capi.RT_FLAG_SUN if args.sun else 0
     rows = []
+    jobs = []
     for cname in args.configs.split(","):
         cfg = scenes.CONFIGS[cname]
+        for dep in ([int(x) for x in args.depths.split(",")] if args.depths else [cfg.depth]):
+            jobs.append((cname, cfg, dep))
+    for cname, cfg, depth in jobs:
         sc = cfg.scene()
         rend.set_scene(scenes.to_prims(sc))
         cam = capi.camera_init(**scenes.camera_args(cfg.width, cfg.height))
@@ -49,17 +56,17 @@ def main():
             for p in precs:
                 pc = capi.PRECISIONS[p]
                 if segs is None:
-                    rend.render_device(cam, cfg.depth, out.data_ptr(), pc, flags, 0,
+                    rend.render_device(cam, depth, out.data_ptr(), pc, flags, 0,
                                        d_segments=segs_t.data_ptr(), stream=stream.cuda_stream)
                     torch.cuda.synchronize()
                     segs = int(segs_t.item())
                 for _ in range(2):
-                    rend.render_device(cam, cfg.depth, out.data_ptr(), pc, flags, 0,
+                    rend.render_device(cam, depth, out.data_ptr(), pc, flags, 0,
                                        stream=stream.cuda_stream)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
                 for _ in range(args.reps):
-                    rend.render_device(cam, cfg.depth, out.data_ptr(), pc, flags, 0,
+                    rend.render_device(cam, depth, out.data_ptr(), pc, flags, 0,
                                        stream=stream.cuda_stream)
                 e1.record(stream)
                 torch.cuda.synchronize()
@@ -67,14 +74,14 @@ def main():
         # diagnostic: cull selectivity (one extra launch with counters on)
         st = torch.zeros(3, dtype=torch.int64, device=dev)
         rend.set_option(capi.RT_OPT_STATS_DEVICE_PTR, st.data_ptr())
-        rend.render_device(cam, cfg.depth, out.data_ptr(), capi.PRECISIONS[precs[0]], flags, 0,
+        rend.render_device(cam, depth, out.data_ptr(), capi.PRECISIONS[precs[0]], flags, 0,
                            stream=stream.cuda_stream)
         torch.cuda.synchronize()
         rend.set_option(capi.RT_OPT_STATS_DEVICE_PTR, 0)
         culls, kept, considered = (int(v) for v in st.tolist())
         for p in precs:
             ms = min(times[p])
-            r = dict(config=cname, precision=p, cull=args.cull, ms_min=round(ms, 4),
+            r = dict(config=cname, depth=depth, precision=p, cull=args.cull, eye=args.eye, ms_min=round(ms, 4),
                      ms_med=round(sorted(times[p])[len(times[p]) // 2], 4), segments=segs,
                      grays=round(segs / (ms * 1e-3) / 1e9, 3), culls=culls,
                      kept_frac=round(kept / considered, 4) if considered else None)
