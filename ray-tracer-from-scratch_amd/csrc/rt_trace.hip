@@ -56,6 +56,15 @@
 #ifndef RT_TERMINAL_F32    // PATH64: the last segment of a path (sky, or the hit at max
 #define RT_TERMINAL_F32 1  // depth) feeds colour only, so its normalisations run in fp32
 #endif
+#ifndef RT_WPE_PATH64           // occupancy targets (waves_per_eu below), A/B knobs
+#define RT_WPE_PATH64 4
+#endif
+#ifndef RT_WPE_PATH64_LIN_BONUS
+#define RT_WPE_PATH64_LIN_BONUS 0
+#endif
+#ifndef RT_WPE_F64_LIN_BONUS
+#define RT_WPE_F64_LIN_BONUS 0
+#endif
 #ifndef RT_F32_READLANE   // F32 survivor records: 1 = v_readlane from the culling lane,
 #define RT_F32_READLANE 0 // 0 = scalar loads (A/B: c5 -13%); fp64 paths keep v_readlane
 #endif
@@ -1015,10 +1024,12 @@ constexpr int waves_per_eu() {
     // non-integer-exponent deep fp64 variants run at 2 waves and may spill a little).
     const int tier = MAXD >= 16 ? 2 : (MAXD >= 10 ? 1 : 0);
     int w = 0;
+    if (PREC == PREC_F64 && !CULL && !SUN && tier == 0) return 4 + RT_WPE_F64_LIN_BONUS;
     if (PREC == PREC_F32)
         w = 5 - (tier > 0 ? 1 : 0) - ((SUN && tier == 2) ? 1 : 0);
     else if (PREC == PREC_PATH64)
-        w = 4 - (tier == 2 ? 1 : 0) - ((SUN && tier > 0) ? 1 : 0);
+        w = RT_WPE_PATH64 - (tier == 2 ? 1 : 0) - ((SUN && tier > 0) ? 1 : 0) +
+            ((!CULL && !SUN && tier == 0) ? RT_WPE_PATH64_LIN_BONUS : 0);
     else
         w = (INT_EXP ? (SUN ? 3 : 4) : (SUN ? 2 : 3)) - (tier > 0 ? 1 : 0) -
             ((PREC == PREC_MIXED && CULL && MAXD >= 8) ? 1 : 0);  // A/B: F64 faster at 4
