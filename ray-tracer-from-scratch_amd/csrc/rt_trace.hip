@@ -621,6 +621,52 @@ __device__ __forceinline__ f3 local_color_f(const DevMat32& m, float s, float ks
 }
 __device__ __forceinline__ f3 tof(d3 v) { return F3((float)v.x, (float)v.y, (float)v.z); }
 
+/* find_closest_hit for one segment of every live lane: the wave-culled scan (CULL) or the
+ * linear scan.  Converged: every lane of the wave calls it (alive masks the tests). */
+template <bool MIXED, bool CULL>
+__device__ __forceinline__ HitD scan_d(const KParams& p, const RayD& r, bool alive,
+                                       bool primary) {
+    HitD h = no_hit();
+    if (CULL) {
+        // walls first: their distances then bound the sphere tests
+        RayF rf;
+        if (MIXED) rf = make_rayf(r);
+        if (RT_WALLS_FIRST && alive) walls_d<MIXED>(p, r, rf, h);
+        const Cone cn = wave_cone(F3((float)r.o.x, (float)r.o.y, (float)r.o.z),
+                                  F3((float)r.d.x, (float)r.d.y, (float)r.d.z), alive);
+        for (int c0 = 0; c0 < p.nS; c0 += 64) {
+            float lb;
+            SphRec rec;
+            uint64_t m = cull_chunk<true>(p, cn, c0, &lb, rec);
+            // survivors in index order; each record comes out of the testing lane's
+            // registers (v_readlane), no memory round trip
+            while (m) {
+                const int l = __builtin_ctzll(m);
+                m &= m - 1;
+                const double bound = (double)lane_f(lb, l);
+                // exact skip: the sphere's distance is >= bound > this lane's best
+                if (alive && bound <= h.dist) {
+                    const int sidx = c0 + l;
+                    const float Sf[4] = {lane_f(rec.f[0], l), lane_f(rec.f[1], l),
+                                         lane_f(rec.f[2], l), lane_f(rec.f[3], l)};
+                    if (!(MIXED && sphere_cull(Sf, rf))) {
+                        const double Sd[4] = {lane_d(rec.d[0], l), lane_d(rec.d[1], l),
+                                              lane_d(rec.d[2], l), lane_d(rec.d[3], l)};
+                        sphere_exact<false>(Sd, sidx, r, h, &p);
+                    }
+                }
+            }
+        }
+        if (!RT_WALLS_FIRST && alive) walls_d<MIXED>(p, r, rf, h);
+    } else if (alive) {
+        // primary and p.eye are wave-uniform: one scan or the other per wave (MIXED
+        // keeps its fp32 cull in front of every test: no eye tables, A/B +1.5%)
+        h = (!MIXED && primary && p.eye) ? closest_hit_d<MIXED, true>(p, r)
+                              : closest_hit_d<MIXED, false>(p, r);
+    }
+    return h;
+}
+
 /* One pixel on the exact fp64 ray path.  COLOR64: colour arithmetic in fp64 too (F64 /
  * MIXED, the parity modes); otherwise in fp32 (PATH64). */
 template <bool MIXED, bool COLOR64, bool SUN, bool INT_EXP, bool CULL, int MAXD>
@@ -642,44 +688,7 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
     // reduce over its live rays; k is wave-uniform.
     for (int k = 0;; ++k) {
         if (!__any(alive)) break;
-        HitD h = no_hit();
-        if (CULL) {
-            // walls first: their distances then bound the sphere tests
-            RayF rf;
-            if (MIXED) rf = make_rayf(r);
-            if (RT_WALLS_FIRST && alive) walls_d<MIXED>(p, r, rf, h);
-            const Cone cn = wave_cone(F3((float)r.o.x, (float)r.o.y, (float)r.o.z),
-                                      F3((float)r.d.x, (float)r.d.y, (float)r.d.z), alive);
-            for (int c0 = 0; c0 < p.nS; c0 += 64) {
-                float lb;
-                SphRec rec;
-                uint64_t m = cull_chunk<true>(p, cn, c0, &lb, rec);
-                // survivors in index order; each record comes out of the testing lane's
-                // registers (v_readlane), no memory round trip
-                while (m) {
-                    const int l = __builtin_ctzll(m);
-                    m &= m - 1;
-                    const double bound = (double)lane_f(lb, l);
-                    // exact skip: the sphere's distance is >= bound > this lane's best
-                    if (alive && bound <= h.dist) {
-                        const int sidx = c0 + l;
-                        const float Sf[4] = {lane_f(rec.f[0], l), lane_f(rec.f[1], l),
-                                             lane_f(rec.f[2], l), lane_f(rec.f[3], l)};
-                        if (!(MIXED && sphere_cull(Sf, rf))) {
-                            const double Sd[4] = {lane_d(rec.d[0], l), lane_d(rec.d[1], l),
-                                                  lane_d(rec.d[2], l), lane_d(rec.d[3], l)};
-                            sphere_exact<false>(Sd, sidx, r, h, &p);
-                        }
-                    }
-                }
-            }
-            if (!RT_WALLS_FIRST && alive) walls_d<MIXED>(p, r, rf, h);
-        } else if (alive) {
-            // k == 0 and p.eye are wave-uniform: one scan or the other per wave (MIXED
-            // keeps its fp32 cull in front of every test: no eye tables, A/B +1.5%)
-            h = (!MIXED && k == 0 && p.eye) ? closest_hit_d<MIXED, true>(p, r)
-                                  : closest_hit_d<MIXED, false>(p, r);
-        }
+        const HitD h = scan_d<MIXED, CULL>(p, r, alive, k == 0);
         if (!alive) continue;
         ++segs;
         const bool last = k >= p.depth || k >= MAXD;  // remaining_iterations <= 0 (main.cpp:105)
@@ -989,9 +998,8 @@ __device__ __forceinline__ unsigned q8(double v) {
     return (unsigned)(v * 255.0);
 }
 
-__device__ __forceinline__ void store_pixel(const KParams& p, int r, int x, double cr, double cg,
-                                            double cb) {
-    const size_t px = (size_t)r * (size_t)p.W + (size_t)x;
+__device__ __forceinline__ void store_px(const KParams& p, size_t px, double cr, double cg,
+                                         double cb) {
     if (p.outf == OUT_RGB_F32) {
         float* o = static_cast<float*>(p.out) + px * 3;
         o[0] = (float)cr;
@@ -1006,6 +1014,10 @@ __device__ __forceinline__ void store_pixel(const KParams& p, int r, int x, doub
         const unsigned v = q8(cr) | (q8(cg) << 8) | (q8(cb) << 16) | (255u << 24);
         static_cast<unsigned*>(p.out)[px] = v;
     }
+}
+__device__ __forceinline__ void store_pixel(const KParams& p, int r, int x, double cr, double cg,
+                                            double cb) {
+    store_px(p, (size_t)r * (size_t)p.W + (size_t)x, cr, cg, cb);
 }
 
 __device__ __forceinline__ void count_segments(const KParams& p, int segs) {
