@@ -56,6 +56,24 @@
 #ifndef RT_TERMINAL_F32    // PATH64: the last segment of a path (sky, or the hit at max
 #define RT_TERMINAL_F32 1  // depth) feeds colour only, so its normalisations run in fp32
 #endif
+#ifndef RT_DIAG            // diagnostic build: count wave/lane entries of branch bodies
+#define RT_DIAG 0          // into g_diag (rt_diag_read); never on in the product
+#endif
+#if RT_DIAG
+__device__ unsigned long long g_diag[16];
+#define DIAG(i)                                                                     \
+    do {                                                                            \
+        const uint64_t b_ = __ballot(1);                                            \
+        if ((uint64_t)__lane_id() == (uint64_t)__builtin_ctzll(b_)) {                \
+            atomicAdd(&g_diag[(i)], 1ull);                                          \
+            atomicAdd(&g_diag[(i) + 1], (unsigned long long)__popcll(b_));          \
+        }                                                                           \
+    } while (0)
+#else
+#define DIAG(i) \
+    do {        \
+    } while (0)
+#endif
 #ifndef RT_WPE_PATH64           // occupancy targets (waves_per_eu below), A/B knobs
 #define RT_WPE_PATH64 4
 #endif
@@ -233,6 +251,7 @@ __device__ __forceinline__ void sphere_exact_oc(const d3 oc, const double c, int
     if (dt > 0) return;
     const double x = dt * dt - r.a * c;  // det / 4
     if (!(x >= 0)) return;
+    DIAG(2);
     double proj, pt;
     if (x == 0) {
         pt = div_r(-dt, r.a, r.ra);  // -b / (2a)
@@ -270,9 +289,11 @@ __device__ __forceinline__ void wall_exact(const Wall64& Wl, int w, const KParam
     const double den = dot(n, r.d);
     const double num = EYE ? p.eye_w[w] : dot(P - r.o, n);
     if (!((num > 0 && den > 0) || (num < 0 && den < 0))) return;
+    DIAG(4);
     const double t = div_r(num, den, rcp_refined(den));
     if (!(t > 0)) return;
     if (RT_WALL_TSKIP && t > h.dist) return;  // loses to the current best either way
+    DIAG(6);
     const d3 q = (r.o + r.d * t) - P;  // ray::at (scene.h:16) minus the corner
     const double px = dot(q, ld3(Wl.X));
     const double py = dot(q, ld3(Wl.Y));
@@ -498,6 +519,7 @@ __device__ __forceinline__ void walls_d(const KParams& p, const RayD& r, const R
  * segment, origin terms from the eye tables (rt_device.h). */
 template <bool MIXED, bool EYE>
 __device__ __forceinline__ HitD closest_hit_d(const KParams& p, const RayD& r) {
+    DIAG(0);
     HitD h = no_hit();
     RayF rf;
     if (MIXED) rf = make_rayf(r);
@@ -694,6 +716,7 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
         const bool last = k >= p.depth || k >= MAXD;  // remaining_iterations <= 0 (main.cpp:105)
         if (!COLOR64 && RT_TERMINAL_F32 && (last || h.slot < 0)) {
             // PATH64, last segment of the path: nothing here feeds another ray
+            DIAG(10);
             const f3 d32 = tof(r.d);
             const f3 nv32 = fnormalize(d32);
             if (h.slot < 0) {
@@ -720,6 +743,7 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
             alive = false;
             continue;
         }
+        DIAG(8);
         const double rdl = rcp_refined(r.dlen);
         const d3 nv = div3(r.d, r.dlen, rdl);  // normalize(d); normalize(-d) == -nv
         if (h.slot < 0) {
@@ -1108,6 +1132,15 @@ static hipError_t launch_prec(const KParams& p, dim3 grid, hipStream_t st) {
 }
 
 int max_depth() { return MAXD_LARGE; }
+
+#if RT_DIAG
+extern "C" int rt_diag_read(unsigned long long* out16) {
+    const int e = (int)hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_diag), sizeof g_diag);
+    unsigned long long z[16] = {0};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_diag), z, sizeof z);
+    return e;
+}
+#endif
 
 int launch_trace(const KParams& p, int prec, void* stream) {
     if (p.W <= 0 || p.nrows <= 0) return (int)hipSuccess;
