@@ -218,6 +218,7 @@ def main() -> int:
     kernel_ms = ek0.elapsed_time(ek1) / nk
 
     sweep = {}
+    sun_ext = None
     if rank == 0 and not args.no_sweep:
         for pname, pc in capi.PRECISIONS.items():
             e0 = torch.cuda.Event(enable_timing=True)
@@ -234,6 +235,25 @@ def main() -> int:
             sweep[pname] = {"kernel_ms": round(kms, 4),
                             "mrays_per_s": round(my_segs / (kms * 1e-3) / 1e6, 1),
                             "dtype": DTYPE[pname], "parity": PARITY[pname]}
+        if not args.sun:
+            # config 2's "sun" is reported as a separate extension run (same ray
+            # paths and segment count; the sun only adds shading terms)
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            rend.render_device(cam, depth, out.data_ptr(), prec, capi.RT_FLAG_SUN,
+                               capi.RT_OUT_RGB_F32, row0=row0, nrows=nrows, stream=stream.cuda_stream)
+            e0.record(stream)
+            for _ in range(nk):
+                rend.render_device(cam, depth, out.data_ptr(), prec, capi.RT_FLAG_SUN,
+                                   capi.RT_OUT_RGB_F32, row0=row0, nrows=nrows,
+                                   stream=stream.cuda_stream)
+            e1.record(stream)
+            torch.cuda.synchronize(dev)
+            kms = e0.elapsed_time(e1) / nk
+            sun_ext = {"precision": args.precision, "kernel_ms": round(kms, 4),
+                       "mrays_per_s": round(my_segs / (kms * 1e-3) / 1e6, 1),
+                       "parity": "sun term is build-defined (constants main.cpp:18-19, unused "
+                                 "by the reference): pinned to the oracle, not the reference"}
 
     result = None
     if rank == 0:
@@ -299,6 +319,7 @@ def main() -> int:
             },
             "cpu_baseline": None,
             "precision_sweep": sweep or None,
+            "sun_extension": sun_ext,
         }
         if world == 1 and not args.no_cpu_baseline and args.cpu_seconds > 0:
             result["cpu_baseline"] = cpu_baseline(cfg, prims, cam, depth, flags, args.cpu_seconds)
