@@ -138,9 +138,13 @@ enum rt_option {
     RT_OPT_STATS_DEVICE_PTR = 2,      /* diagnostics: device address of 3 uint64 counters
                                          that renders add to ([0] wave culls, [1] spheres
                                          kept, [2] spheres considered); 0 = off */
-    RT_OPT_EYE_TABLES = 3             /* 1 (default): primary rays use per-frame tables of
+    RT_OPT_EYE_TABLES = 3,            /* 1 (default): primary rays use per-frame tables of
                                          their camera-origin terms (small scenes); 0 = off.
                                          Output is identical. */
+    RT_OPT_TILE_BINS = 4              /* 1 (default): a per-frame pre-pass proves, per 8x8
+                                         tile, which primitives no primary ray of the tile
+                                         can hit (scenes of <= 64 primitives, exact
+                                         precisions); 0 = off.  Output is identical. */
 };
 int rt_set_option(rt_ctx* ctx, int32_t option, int64_t value);
 

@@ -28,12 +28,13 @@ struct rt_ctx {
     unsigned long long* d_stats = nullptr;
     int wave_cull_min = 24;  // spheres from which the wave cull pays (tools/sweep.py)
     bool eye_tables = true;  // RT_OPT_EYE_TABLES
+    bool tile_bins = true;   // RT_OPT_TILE_BINS
     size_t off_s64 = 0, off_w32 = 0, off_w64 = 0, off_sj = 0, off_wj = 0, off_mat = 0, off_mat32 = 0;
     void* d_out = nullptr;
     size_t d_out_cap = 0;
     unsigned long long* d_segs = nullptr;
-    std::vector<double> h_sph;  // host copy: nS x {cx, cy, cz, radius^2}
-    std::vector<double> h_wal;  // host copy: nW x {P, n}
+    std::vector<double> h_sph;  // host copy: nS x {cx, cy, cz, radius^2, radius}
+    std::vector<double> h_wal;  // host copy: nW x {P, n, X, Y, length, width}
     char last_err[256] = {0};
 };
 
@@ -88,6 +89,173 @@ int check_render_args(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, int
     return RT_OK;
 }
 
+/* ---- primary-ray tile bins (rt_device.h PrimBox) -------------------------------------
+ * A point X = o + u*d(x, i) of a primary ray has (u, u*x, u*i) = M^-1 (X - o) with
+ * M = [o - TL, -dx, -dy] (columns), d(x, i) = o - (TL + dx*x + dy*i) (main.cpp:132-133).
+ * The box of a convex hull is the box of its projected vertices (the map is projective,
+ * convexity-preserving on u > 0), floor/ceil'd and widened by one pixel.  Conditions
+ * that make the box a proof (DESIGN.md §3 "tile bins"):
+ *   - a primitive is only boxed when the camera is clearly off it (sphere: |o - C| >
+ *     r*sqrt(3) + delta; wall: |num| = |(P - o).n| > 1e-9 * scale, below which rounding of
+ *     a near-grazing ray's t could be arbitrary), otherwise it keeps every tile;
+ *   - hull entirely at u < 0: the line meets it behind the camera only (t < 0), never;
+ *   - wall polygon clipped to u >= eps = |num| / (2 max|d|): hits at u < eps would lie
+ *     closer to o than the wall's plane, impossible;
+ *   - a sphere hull straddling u = 0 keeps every tile.
+ * Outside the box by >= 1 pixel the exact ray misses the hull by an angle of ~1 pixel
+ * while the reference's rounding moves a hit by ~1e-13 pixel (both scale alike with the
+ * grazing angle), so the reference's test rejects the primitive as well. */
+struct Proj {
+    double r[3][3];  // rows of M^-1
+    double o[3];
+};
+inline double dot3(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+inline void cross3(const double* a, const double* b, double* c) {
+    c[0] = a[1] * b[2] - a[2] * b[1];
+    c[1] = a[2] * b[0] - a[0] * b[2];
+    c[2] = a[0] * b[1] - a[1] * b[0];
+}
+bool make_proj(const rt_camera* cam, Proj& P) {
+    double e[3], c1[3], c2[3];
+    for (int k = 0; k < 3; k++) {
+        P.o[k] = cam->position[k];
+        e[k] = cam->position[k] - cam->image_top_left[k];
+        c1[k] = -cam->pixel_delta_x[k];
+        c2[k] = -cam->pixel_delta_y[k];
+    }
+    double x12[3], x20[3], x01[3];
+    cross3(c1, c2, x12);
+    cross3(c2, e, x20);
+    cross3(e, c1, x01);
+    const double det = dot3(e, x12);
+    if (!(std::fabs(det) > 0) || !std::isfinite(det)) return false;
+    for (int k = 0; k < 3; k++) {
+        P.r[0][k] = x12[k] / det;
+        P.r[1][k] = x20[k] / det;
+        P.r[2][k] = x01[k] / det;
+    }
+    return true;
+}
+inline double proj_u(const Proj& P, const double* X) {
+    const double v[3] = {X[0] - P.o[0], X[1] - P.o[1], X[2] - P.o[2]};
+    return dot3(P.r[0], v);
+}
+struct BoxAcc {
+    double x0 = INFINITY, x1 = -INFINITY, i0 = INFINITY, i1 = -INFINITY;
+    bool bad = false;
+    void add(const Proj& P, const double* X) {
+        const double v[3] = {X[0] - P.o[0], X[1] - P.o[1], X[2] - P.o[2]};
+        const double u = dot3(P.r[0], v);
+        const double x = dot3(P.r[1], v) / u, i = dot3(P.r[2], v) / u;
+        if (!std::isfinite(x) || !std::isfinite(i) || !(u > 0)) bad = true;
+        x0 = std::fmin(x0, x);
+        x1 = std::fmax(x1, x);
+        i0 = std::fmin(i0, i);
+        i1 = std::fmax(i1, i);
+    }
+};
+
+void frame_boxes(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nrows,
+                 rt::KParams& p) {
+    p.nbox = 0;
+    const int np = ctx->nS + ctx->nW;
+    if (!ctx->tile_bins || p.wave_cull || np == 0 || np > rt::BIN_MAX_PRIMS || cam->width > 32000 ||
+        cam->height > 32000 || nrows <= 0 || cam->width <= 0)
+        return;
+    Proj P;
+    if (!make_proj(cam, P)) return;
+    const double W = cam->width, R0 = row0, R1 = row0 + nrows - 1;
+    const rt::PrimBox all{-1, (int16_t)cam->width, (int16_t)(row0 - 1), (int16_t)(row0 + nrows)};
+    const rt::PrimBox none{1, 0, 1, 0};
+    auto to_box = [&](const BoxAcc& b) -> rt::PrimBox {
+        if (b.bad) return all;
+        const double x0 = std::floor(b.x0) - 1, x1 = std::ceil(b.x1) + 1;
+        const double i0 = std::floor(b.i0) - 1, i1 = std::ceil(b.i1) + 1;
+        if (x0 > W - 1 || x1 < 0 || i0 > R1 || i1 < R0) return none;
+        return rt::PrimBox{(int16_t)std::fmax(x0, -1.0), (int16_t)std::fmin(x1, W),
+                           (int16_t)std::fmax(i0, R0 - 1), (int16_t)std::fmin(i1, R1 + 1)};
+    };
+    // largest |d| over the frame: d is affine in (x, i), so at a corner of the pixel grid
+    double dmax = 0;
+    for (int c = 0; c < 4; c++) {
+        const double x = (c & 1) ? W - 1 : 0, i = (c & 2) ? R1 : R0;
+        double d[3];
+        for (int k = 0; k < 3; k++)
+            d[k] = cam->position[k] -
+                   (cam->image_top_left[k] + cam->pixel_delta_x[k] * x + cam->pixel_delta_y[k] * i);
+        dmax = std::fmax(dmax, std::sqrt(dot3(d, d)));
+    }
+    const double* o = cam->position;
+    const double oabs = std::fabs(o[0]) + std::fabs(o[1]) + std::fabs(o[2]);
+    for (int s = 0; s < ctx->nS; s++) {
+        const double* S = &ctx->h_sph[5 * s];
+        const double r = S[4];
+        const double v[3] = {S[0] - o[0], S[1] - o[1], S[2] - o[2]};
+        const double delta = 1e-6 * (1 + oabs + std::fabs(S[0]) + std::fabs(S[1]) + std::fabs(S[2]) + r);
+        rt::PrimBox b = all;
+        if (std::sqrt(dot3(v, v)) > r * 1.7320508075688772 + delta && r > 1e-9 * std::sqrt(dot3(v, v))) {
+            double umin = INFINITY, umax = -INFINITY;
+            double X[8][3];
+            for (int c = 0; c < 8; c++) {
+                for (int k = 0; k < 3; k++) X[c][k] = S[k] + (((c >> k) & 1) ? r : -r);
+                const double u = proj_u(P, X[c]);
+                umin = std::fmin(umin, u);
+                umax = std::fmax(umax, u);
+            }
+            if (umax < 0) {
+                b = none;
+            } else if (umin > 0) {
+                BoxAcc acc;
+                for (int c = 0; c < 8; c++) acc.add(P, X[c]);
+                b = to_box(acc);
+            }
+        }
+        p.box[s] = b;
+    }
+    for (int w = 0; w < ctx->nW; w++) {
+        const double* Wd = &ctx->h_wal[14 * w];
+        const double *Pw = Wd, *n = Wd + 3, *X = Wd + 6, *Y = Wd + 9;
+        const double len = Wd[12], wid = Wd[13];
+        const double pv[3] = {Pw[0] - o[0], Pw[1] - o[1], Pw[2] - o[2]};
+        const double num = dot3(pv, n);
+        const double scale = 1 + oabs + std::fabs(Pw[0]) + std::fabs(Pw[1]) + std::fabs(Pw[2]) + len + wid;
+        rt::PrimBox b = all;
+        if (std::fabs(num) > 1e-9 * scale && dmax > 0) {
+            double V[4][3];  // P, P + len X, P + len X + wid Y, P + wid Y (cyclic)
+            for (int k = 0; k < 3; k++) {
+                V[0][k] = Pw[k];
+                V[1][k] = Pw[k] + X[k] * len;
+                V[2][k] = Pw[k] + X[k] * len + Y[k] * wid;
+                V[3][k] = Pw[k] + Y[k] * wid;
+            }
+            double u[4], umax = -INFINITY;
+            for (int c = 0; c < 4; c++) {
+                u[c] = proj_u(P, V[c]);
+                umax = std::fmax(umax, u[c]);
+            }
+            const double eps = 0.5 * std::fabs(num) / dmax;
+            if (umax < eps) {
+                b = none;  // every point behind the camera or closer than the wall's plane
+            } else {
+                BoxAcc acc;  // Sutherland-Hodgman against u >= eps
+                for (int c = 0; c < 4; c++) {
+                    const int c2 = (c + 1) & 3;
+                    if (u[c] >= eps) acc.add(P, V[c]);
+                    if ((u[c] >= eps) != (u[c2] >= eps)) {
+                        const double t = (eps - u[c]) / (u[c2] - u[c]);
+                        double Xc[3];
+                        for (int k = 0; k < 3; k++) Xc[k] = V[c][k] + (V[c2][k] - V[c][k]) * t;
+                        acc.add(P, Xc);
+                    }
+                }
+                b = to_box(acc);
+            }
+        }
+        p.box[ctx->nS + w] = b;
+    }
+    p.nbox = np;
+}
+
 rt::KParams make_params(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nrows,
                         int32_t depth, uint32_t flags, int32_t out_format, void* d_out,
                         unsigned long long* d_segs) {
@@ -126,18 +294,19 @@ rt::KParams make_params(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, i
     if (p.eye) {
         const double* o = cam->position;
         for (int s = 0; s < ctx->nS; s++) {
-            const double* S = &ctx->h_sph[4 * s];
+            const double* S = &ctx->h_sph[5 * s];
             const double ox = o[0] - S[0], oy = o[1] - S[1], oz = o[2] - S[2];  // scene.cpp:45
             const double c = (ox * ox + oy * oy + oz * oz) - S[3];              // scene.cpp:51
             const double e[4] = {ox, oy, oz, c};
             for (int k = 0; k < 4; k++) p.eye_s[s][k] = e[k];
         }
         for (int w = 0; w < ctx->nW; w++) {
-            const double* P = &ctx->h_wal[6 * w];
+            const double* P = &ctx->h_wal[14 * w];
             const double* n = P + 3;
             p.eye_w[w] = (P[0] - o[0]) * n[0] + (P[1] - o[1]) * n[1] + (P[2] - o[2]) * n[2];  // scene.cpp:10
         }
     }
+    frame_boxes(ctx, cam, row0, nrows, p);
     return p;
 }
 
@@ -374,15 +543,22 @@ int rt_set_scene(rt_ctx* ctx, const rt_prim* prims, int32_t n) {
         const double e = mat[k].ex;
         if (!(e >= 0.0 && e <= 1024.0 && e == std::floor(e))) ctx->int_exp = false;
     }
-    ctx->h_sph.assign(4 * nS, 0.0);
-    for (size_t s = 0; s < nS; s++)
-        for (int k = 0; k < 4; k++) ctx->h_sph[4 * s + k] = s64[s / 4].v[s % 4][k];
-    ctx->h_wal.assign(6 * nW, 0.0);
-    for (size_t w = 0; w < nW; w++)
+    ctx->h_sph.assign(5 * nS, 0.0);
+    for (size_t s = 0; s < nS; s++) {
+        for (int k = 0; k < 4; k++) ctx->h_sph[5 * s + k] = s64[s / 4].v[s % 4][k];
+        ctx->h_sph[5 * s + 4] = sph[s].r;
+    }
+    ctx->h_wal.assign(14 * nW, 0.0);
+    for (size_t w = 0; w < nW; w++) {
         for (int k = 0; k < 3; k++) {
-            ctx->h_wal[6 * w + k] = w64[w].P[k];
-            ctx->h_wal[6 * w + 3 + k] = w64[w].n[k];
+            ctx->h_wal[14 * w + k] = w64[w].P[k];
+            ctx->h_wal[14 * w + 3 + k] = w64[w].n[k];
+            ctx->h_wal[14 * w + 6 + k] = w64[w].X[k];
+            ctx->h_wal[14 * w + 9 + k] = w64[w].Y[k];
         }
+        ctx->h_wal[14 * w + 12] = w64[w].len;
+        ctx->h_wal[14 * w + 13] = w64[w].wid;
+    }
     ctx->off_s64 = off_s64;
     ctx->off_w32 = off_w32;
     ctx->off_w64 = off_w64;
@@ -408,6 +584,10 @@ int rt_set_option(rt_ctx* ctx, int32_t option, int64_t value) {
             if (value != 0 && value != 1) return RT_ERR_INVALID_ARG;
             ctx->eye_tables = value == 1;
             return RT_OK;
+        case RT_OPT_TILE_BINS:
+            if (value != 0 && value != 1) return RT_ERR_INVALID_ARG;
+            ctx->tile_bins = value == 1;
+            return RT_OK;
         default:
             return RT_ERR_INVALID_ARG;
     }
@@ -432,8 +612,8 @@ int rt_render_device(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nr
     int st = check_render_args(ctx, cam, row0, nrows, depth, precision, out_format);
     if (st != RT_OK) return st;
     if (!d_out && nrows > 0 && cam->width > 0) return RT_ERR_INVALID_ARG;
-    const rt::KParams p = make_params(ctx, cam, row0, nrows, depth, flags, out_format, d_out,
-                                      reinterpret_cast<unsigned long long*>(d_segments));
+    rt::KParams p = make_params(ctx, cam, row0, nrows, depth, flags, out_format, d_out,
+                                reinterpret_cast<unsigned long long*>(d_segments));
     void* s = stream ? stream : static_cast<void*>(ctx->stream);
     const int e = rt::launch_trace(p, precision, s);
     if (e != (int)hipSuccess) return hip_fail(ctx, (hipError_t)e, "launch k_trace");
@@ -458,9 +638,9 @@ int rt_render(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nrows, in
     }
     unsigned long long* segs = count_segments ? ctx->d_segs : nullptr;
     if (segs) RT_HIP(ctx, hipMemsetAsync(segs, 0, sizeof *segs, ctx->stream));
+    rt::KParams p = make_params(ctx, cam, row0, nrows, depth, flags, out_format,
+                                ctx->d_out, segs);
     RT_HIP(ctx, hipEventRecord(ctx->ev0, ctx->stream));
-    const rt::KParams p = make_params(ctx, cam, row0, nrows, depth, flags, out_format,
-                                      ctx->d_out, segs);
     const int e = rt::launch_trace(p, precision, ctx->stream);
     if (e != (int)hipSuccess) return hip_fail(ctx, (hipError_t)e, "launch k_trace");
     RT_HIP(ctx, hipEventRecord(ctx->ev1, ctx->stream));

@@ -83,6 +83,21 @@ constexpr int TILE_H = RT_WAVES_PER_BLOCK >= 4 ? 16 : 8;
 constexpr int EYE_MAX_S = 32;
 constexpr int EYE_MAX_W = 16;
 
+// Primary-ray tile bins.  Every primary ray starts at the camera o with direction
+// d(x, i) = o - (TL + dx*x + dy*i) (main.cpp:132-133), so a point X = o + u*d(x, i) has
+// pixel coordinates (x, i) = (p/u, q/u) where (u, p, q) = M^-1 (X - o), M = [o - TL, -dx,
+// -dy]: a projective map.  Per frame the host projects each primitive's convex hull (a
+// sphere's bounding cube, a wall's rectangle clipped to u >= eps) to a pixel bounding box
+// widened by one pixel (rt_capi.cpp frame_boxes); the kernel ANDs its 8x8 tile against
+// the boxes (one lane per primitive, one ballot) and the primary scan tests only the
+// primitives whose box meets the tile.  A primitive outside the box by >= 1 pixel is
+// missed by the exact ray by an angle ~1e12 times the reference's rounding, so the
+// reference's own test rejects it too.  Scenes of <= 64 primitives.
+constexpr int BIN_MAX_PRIMS = 64;
+struct PrimBox {
+    int16_t x0, x1, i0, i1;  // inclusive pixel box (frame rows); x0 > x1 = never hit
+};
+
 struct KParams {
     const SphG32* s32;
     const SphG64* s64;
@@ -102,6 +117,9 @@ struct KParams {
     void* out;
     unsigned long long* segs;   // may be null
     unsigned long long* stats;  // diagnostic counters, may be null (rt_set_option)
+    int32_t nbox;               // primitives with a PrimBox (nS + nW), 0 = tile bins off
+    int32_t pad_box;
+    PrimBox box[BIN_MAX_PRIMS]; // material-slot order: spheres, then walls
     int32_t eye;                        // eye tables below valid
     int32_t pad_eye;
     double eye_s[EYE_MAX_S][4];         // sphere s: {oc.x, oc.y, oc.z, |oc|^2 - r^2}

@@ -560,6 +560,36 @@ __device__ __forceinline__ HitD closest_hit_d(const KParams& p, const RayD& r) {
     return h;
 }
 
+/* Primary segment behind the tile bins (rt_device.h PrimBox): only the primitives whose
+ * pixel box meets the wave's tile are tested, spheres in increasing index (the strict-<
+ * tie rule holds: a skipped sphere cannot hit), then walls.  keep is wave-uniform. */
+template <bool MIXED, bool EYE>
+__device__ __forceinline__ HitD closest_hit_bin(const KParams& p, const RayD& r, uint64_t keep) {
+    DIAG(0);
+    HitD h = no_hit();
+    RayF rf;
+    if (MIXED) rf = make_rayf(r);
+    uint64_t sm = p.nS >= 64 ? keep : keep & ((1ull << p.nS) - 1);
+    while (sm) {
+        const int s = __builtin_ctzll(sm);
+        sm &= sm - 1;
+        if (EYE) {
+            const double* E = p.eye_s[s];
+            sphere_exact_oc(D3(E[0], E[1], E[2]), E[3], s, r, h);
+        } else {
+            sphere_by_index<MIXED>(p, s, r, rf, h);
+        }
+    }
+    uint64_t wm = p.nS >= 64 ? 0 : keep >> p.nS;
+    while (wm) {
+        const int w = __builtin_ctzll(wm);
+        wm &= wm - 1;
+        if (MIXED && wall_cull(p.w32[w], rf)) continue;
+        wall_exact<EYE>(p.w64[w], w, p, r, h);
+    }
+    return h;
+}
+
 /* out_color, main.cpp:28-37: only normalize(v).z is used; z^0.25 as sqrt(sqrt(z)). */
 __device__ __forceinline__ d3 sky_d(const RayD& r, double nvz) {
     if (r.d.z < 0.0) return ground_color();
@@ -643,11 +673,31 @@ __device__ __forceinline__ f3 local_color_f(const DevMat32& m, float s, float ks
 }
 __device__ __forceinline__ f3 tof(d3 v) { return F3((float)v.x, (float)v.y, (float)v.z); }
 
+__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+/* The primitives whose pixel box meets this wave's 8x8 tile (rt_device.h PrimBox): lane l
+ * tests box l, one ballot.  Call with every lane active. */
+__device__ __forceinline__ uint64_t tile_keep(const KParams& p) {
+    const int wave = threadIdx.x >> 6;
+    const int tx0 = blockIdx.x * TILE_W + (TILE_W > 8 ? (wave & 1) * 8 : 0);
+    const int ty0 = p.row0 + blockIdx.y * TILE_H + (TILE_H > 8 ? (wave >> 1) * 8 : 0);
+    const int l = threadIdx.x & 63;
+    bool hit = false;
+    if (l < p.nbox) {
+        const PrimBox b = p.box[l];
+        hit = b.x0 <= tx0 + 7 && b.x1 >= tx0 && b.i0 <= ty0 + 7 && b.i1 >= ty0;
+    }
+    return uniform64(__ballot(hit));
+}
+
 /* find_closest_hit for one segment of every live lane: the wave-culled scan (CULL) or the
  * linear scan.  Converged: every lane of the wave calls it (alive masks the tests). */
 template <bool MIXED, bool CULL>
 __device__ __forceinline__ HitD scan_d(const KParams& p, const RayD& r, bool alive,
-                                       bool primary) {
+                                       bool primary, uint64_t keep) {
     HitD h = no_hit();
     if (CULL) {
         // walls first: their distances then bound the sphere tests
@@ -681,10 +731,15 @@ __device__ __forceinline__ HitD scan_d(const KParams& p, const RayD& r, bool ali
         }
         if (!RT_WALLS_FIRST && alive) walls_d<MIXED>(p, r, rf, h);
     } else if (alive) {
-        // primary and p.eye are wave-uniform: one scan or the other per wave (MIXED
+        // primary, p.eye and p.bins are wave-uniform: one scan or another per wave (MIXED
         // keeps its fp32 cull in front of every test: no eye tables, A/B +1.5%)
-        h = (!MIXED && primary && p.eye) ? closest_hit_d<MIXED, true>(p, r)
-                              : closest_hit_d<MIXED, false>(p, r);
+        if (primary && p.nbox > 0) {
+            h = (!MIXED && p.eye) ? closest_hit_bin<MIXED, true>(p, r, keep)
+                                  : closest_hit_bin<MIXED, false>(p, r, keep);
+        } else {
+            h = (!MIXED && primary && p.eye) ? closest_hit_d<MIXED, true>(p, r)
+                                             : closest_hit_d<MIXED, false>(p, r);
+        }
     }
     return h;
 }
@@ -699,6 +754,7 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
     const d3 pc = (ld3(p.tl) + ld3(p.dx) * (double)x) + ld3(p.dy) * (double)i;  // main.cpp:132
     RayD r = make_ray(cpos, cpos - pc);  // main.cpp:133-134 (direction not normalised)
     constexpr bool sun = SUN;
+    const uint64_t keep = (!CULL && p.nbox > 0) ? tile_keep(p) : ~0ull;  // all lanes active
 
     CT st_s[MAXD];
     CT st_k[MAXD];
@@ -710,7 +766,7 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
     // reduce over its live rays; k is wave-uniform.
     for (int k = 0;; ++k) {
         if (!__any(alive)) break;
-        const HitD h = scan_d<MIXED, CULL>(p, r, alive, k == 0);
+        const HitD h = scan_d<MIXED, CULL>(p, r, alive, k == 0, keep);
         if (!alive) continue;
         ++segs;
         const bool last = k >= p.depth || k >= MAXD;  // remaining_iterations <= 0 (main.cpp:105)

@@ -46,6 +46,7 @@ RT_FLAG_SUN = 1
 RT_OPT_WAVE_CULL_MIN_SPHERES = 1
 RT_OPT_STATS_DEVICE_PTR = 2
 RT_OPT_EYE_TABLES = 3
+RT_OPT_TILE_BINS = 4
 
 
 class rt_material(C.Structure):

@@ -395,6 +395,58 @@ def test_eye_tables_are_output_invariant(rend, prec):
         rend.set_option(capi.RT_OPT_EYE_TABLES, 1)
 
 
+# ---------------------------------------------------------------- tile bins
+def _random_wall(rng, near=None):
+    nrm = rng.normal(size=3)
+    nrm /= np.linalg.norm(nrm)
+    pos = rng.uniform(-6, 6, 3) if near is None else near + rng.normal(scale=0.05, size=3)
+    return scenes.Wall(scenes.Material(tuple(rng.uniform(0, 1, 3)), .5), tuple(pos), tuple(nrm),
+                       float(rng.uniform(.5, 8)), float(rng.uniform(.5, 8)))
+
+
+@pytest.mark.parametrize("prec", [capi.RT_PREC_F64, capi.RT_PREC_MIXED, capi.RT_PREC_PATH64])
+def test_tile_bins_are_output_invariant(rend, prec):
+    """The primary-ray tile bins (rt_device.h TileBin, k_bin) only skip primitives the
+    reference's own test rejects for every ray of a tile, and bounds tests it passes:
+    frames with and without them are bitwise identical — random scenes and views, walls
+    through the camera and seen edge-on, wide and narrow fields of view, ragged images,
+    row bands, up to the 64-primitive limit."""
+    rng = np.random.default_rng(31)
+    rend.set_option(capi.RT_OPT_WAVE_CULL_MIN_SPHERES, 2**31 - 1)  # linear scan up to 64 prims
+    try:
+        trials = [(1, 0), (0, 1), (5, 3), (8, 4), (8, 6), (20, 12), (40, 24), (58, 6), (3, 40)]
+        for trial, (ns, nw) in enumerate(trials * 2):
+            sc = scenes.synthetic_scene(ns, min(nw, 6), seed=int(rng.integers(1 << 30)))
+            pos = rng.uniform([-1, -3, -1], [5, 3, 2])
+            for k in range(nw - 6):
+                # some walls pass (almost) through the camera or contain its position
+                sc.append(_random_wall(rng, near=pos if k % 3 == 0 else None))
+            rend.set_scene(scenes.to_prims(sc))
+            vfov = float(rng.choice([20.0, 60.0, 90.0, 150.0, 178.0]))
+            w = int(rng.choice([1, 9, 64, 161, 240]))
+            aspect = float(rng.choice([1.0, 16 / 9, 4 / 3, 0.5]))
+            look = pos + rng.normal(size=3)
+            if trial % 4 == 3:   # axis-aligned view: rays in the walls' planes
+                look = pos + np.array([1.0, 0.0, 0.0])
+            cam = capi.camera_init(pos, look, (0, 0, -1), vfov, aspect, float(w))
+            if cam.height <= 0:
+                continue
+            depth = int(rng.integers(0, 6))
+            r0 = int(rng.integers(0, cam.height))
+            n = int(rng.integers(1, cam.height - r0 + 1))
+            imgs = []
+            for on in (1, 0):
+                rend.set_option(capi.RT_OPT_TILE_BINS, on)
+                img, st = rend.render(cam, depth, prec, 0, capi.RT_OUT_RGB_F64, count_segments=True,
+                                      row0=r0, nrows=n)
+                imgs.append((img, st.segments))
+            assert imgs[0][1] == imgs[1][1], trial
+            assert np.array_equal(imgs[0][0].view(np.uint64), imgs[1][0].view(np.uint64)), trial
+    finally:
+        rend.set_option(capi.RT_OPT_TILE_BINS, 1)
+        rend.set_option(capi.RT_OPT_WAVE_CULL_MIN_SPHERES, 24)
+
+
 # ---------------------------------------------------------------- multi-GPU path (1 rank)
 def test_render_tiled_rccl_single_rank(rend):
     """rtamd.tiling.render_tiled over the nccl (RCCL) backend with one rank: the gathered

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--cull", default="default", help="wave-cull min spheres: default|always|never|N")
     ap.add_argument("--depths", default="", help="comma-separated depths overriding the config's")
     ap.add_argument("--eye", type=int, default=1, help="RT_OPT_EYE_TABLES (0/1)")
+    ap.add_argument("--bins", type=int, default=1, help="RT_OPT_TILE_BINS (0/1)")
     args = ap.parse_args()
     import torch
     dev = torch.device("cuda", 0)
@@ -36,6 +37,7 @@ def main():
     if cull is not None:
         rend.set_option(capi.RT_OPT_WAVE_CULL_MIN_SPHERES, cull)
     rend.set_option(capi.RT_OPT_EYE_TABLES, args.eye)
+    rend.set_option(capi.RT_OPT_TILE_BINS, args.bins)
     flags = capi.RT_FLAG_SUN if args.sun else 0
     rows = []
     jobs = []
