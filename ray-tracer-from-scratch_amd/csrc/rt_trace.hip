@@ -930,8 +930,10 @@ __device__ __forceinline__ void sphere_pair_f(const SphG32& G, int k0, int s0, i
     }
 }
 
-__device__ __forceinline__ void walls_f(const KParams& p, f3 o, f3 d, float& best, int& slot) {
+__device__ __forceinline__ void walls_f(const KParams& p, f3 o, f3 d, float& best, int& slot,
+                                        uint64_t wmask = ~0ull) {
     for (int w = 0; w < p.nW; ++w) {
+        if (w < 64 && !((wmask >> w) & 1)) continue;  // wave-uniform (tile bins)
         const Wall32& Wl = p.w32[w];
         const f3 nw = F3(Wl.n[0], Wl.n[1], Wl.n[2]), P = F3(Wl.P[0], Wl.P[1], Wl.P[2]);
         const float den = fdot(nw, d);
@@ -966,6 +968,7 @@ __device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, bool
     int st_m[MAXD];
     int n = 0;
     f3 c = F3(0.f, 0.f, 0.f);
+    const uint64_t keep = (!CULL && p.nbox > 0) ? tile_keep(p) : ~0ull;  // all lanes active
     for (int k = 0;; ++k) {
         if (!__any(alive)) break;
         const float a = fdot(d, d);
@@ -973,7 +976,20 @@ __device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, bool
         const float rl = frsq(a);
         float best = FLT_MAX, bpt = 0.0f;
         int slot = -1;
-        if (CULL) {
+        if (!CULL && k == 0 && p.nbox > 0) {
+            // primary segment behind the tile bins: kept spheres in index order, kept walls
+            if (alive) {
+                uint64_t sm = p.nS >= 64 ? keep : keep & ((1ull << p.nS) - 1);
+                while (sm) {
+                    const int s = __builtin_ctzll(sm);
+                    sm &= sm - 1;
+                    const SphG32& G = p.s32[s >> 2];
+                    const float Sf[4] = {G.c[0][s & 3], G.c[1][s & 3], G.c[2][s & 3], G.c[3][s & 3]};
+                    sphere_f(Sf, s, o, d, a, ra, rl, best, bpt, slot);
+                }
+                walls_f(p, o, d, best, slot, p.nS >= 64 ? 0 : keep >> p.nS);
+            }
+        } else if (CULL) {
             if (RT_WALLS_FIRST && alive) walls_f(p, o, d, best, slot);
             const Cone cn = wave_cone(o, d, alive);
             for (int c0 = 0; c0 < p.nS; c0 += 64) {
@@ -1018,7 +1034,7 @@ __device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, bool
         }
         if (!alive) continue;
         ++segs;
-        if (!CULL) walls_f(p, o, d, best, slot);
+        if (!CULL && !(k == 0 && p.nbox > 0)) walls_f(p, o, d, best, slot);
         const f3 nv = d * rl;
         if (slot < 0) {
             if (d.z < 0.0f) {

@@ -404,7 +404,8 @@ def _random_wall(rng, near=None):
                        float(rng.uniform(.5, 8)), float(rng.uniform(.5, 8)))
 
 
-@pytest.mark.parametrize("prec", [capi.RT_PREC_F64, capi.RT_PREC_MIXED, capi.RT_PREC_PATH64])
+@pytest.mark.parametrize("prec", [capi.RT_PREC_F64, capi.RT_PREC_MIXED, capi.RT_PREC_PATH64,
+                                  capi.RT_PREC_F32])
 def test_tile_bins_are_output_invariant(rend, prec):
     """The primary-ray tile bins (rt_device.h TileBin, k_bin) only skip primitives the
     reference's own test rejects for every ray of a tile, and bounds tests it passes:
