@@ -155,17 +155,11 @@ struct BoxAcc {
     }
 };
 
-void frame_boxes(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nrows,
-                 rt::KParams& p) {
-    p.nbox = 0;
-    const int np = ctx->nS + ctx->nW;
-    if (!ctx->tile_bins || p.wave_cull || np == 0 || np > rt::BIN_MAX_PRIMS || cam->width > 32000 ||
-        cam->height > 32000 || nrows <= 0 || cam->width <= 0)
-        return;
-    Proj P;
-    if (!make_proj(cam, P)) return;
-    const double W = cam->width, R0 = row0, R1 = row0 + nrows - 1;
-    const rt::PrimBox all{-1, (int16_t)cam->width, (int16_t)(row0 - 1), (int16_t)(row0 + nrows)};
+/* Boxes of every primitive (material-slot order) for the camera P (origin P.o). */
+void boxes_for(const rt_ctx* ctx, const Proj& P, double dmax, int32_t width, int32_t row0,
+               int32_t nrows, rt::PrimBox* out) {
+    const double W = width, R0 = row0, R1 = row0 + nrows - 1;
+    const rt::PrimBox all{-1, (int16_t)width, (int16_t)(row0 - 1), (int16_t)(row0 + nrows)};
     const rt::PrimBox none{1, 0, 1, 0};
     auto to_box = [&](const BoxAcc& b) -> rt::PrimBox {
         if (b.bad) return all;
@@ -175,17 +169,7 @@ void frame_boxes(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t 
         return rt::PrimBox{(int16_t)std::fmax(x0, -1.0), (int16_t)std::fmin(x1, W),
                            (int16_t)std::fmax(i0, R0 - 1), (int16_t)std::fmin(i1, R1 + 1)};
     };
-    // largest |d| over the frame: d is affine in (x, i), so at a corner of the pixel grid
-    double dmax = 0;
-    for (int c = 0; c < 4; c++) {
-        const double x = (c & 1) ? W - 1 : 0, i = (c & 2) ? R1 : R0;
-        double d[3];
-        for (int k = 0; k < 3; k++)
-            d[k] = cam->position[k] -
-                   (cam->image_top_left[k] + cam->pixel_delta_x[k] * x + cam->pixel_delta_y[k] * i);
-        dmax = std::fmax(dmax, std::sqrt(dot3(d, d)));
-    }
-    const double* o = cam->position;
+    const double* o = P.o;
     const double oabs = std::fabs(o[0]) + std::fabs(o[1]) + std::fabs(o[2]);
     for (int s = 0; s < ctx->nS; s++) {
         const double* S = &ctx->h_sph[5 * s];
@@ -210,7 +194,7 @@ void frame_boxes(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t 
                 b = to_box(acc);
             }
         }
-        p.box[s] = b;
+        out[s] = b;
     }
     for (int w = 0; w < ctx->nW; w++) {
         const double* Wd = &ctx->h_wal[14 * w];
@@ -251,9 +235,51 @@ void frame_boxes(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t 
                 b = to_box(acc);
             }
         }
-        p.box[ctx->nS + w] = b;
+        out[ctx->nS + w] = b;
     }
+}
+
+void frame_boxes(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nrows,
+                 rt::KParams& p) {
+    p.nbox = 0;
+    p.nmir = 0;
+    const int np = ctx->nS + ctx->nW;
+    if (!ctx->tile_bins || p.wave_cull || np == 0 || np > rt::BIN_MAX_PRIMS || cam->width > 32000 ||
+        cam->height > 32000 || nrows <= 0 || cam->width <= 0)
+        return;
+    Proj P;
+    if (!make_proj(cam, P)) return;
+    // largest |d| over the frame: d is affine in (x, i), so at a corner of the pixel grid
+    double dmax = 0;
+    for (int c = 0; c < 4; c++) {
+        const double x = (c & 1) ? cam->width - 1 : 0, i = (c & 2) ? row0 + nrows - 1 : row0;
+        double d[3];
+        for (int k = 0; k < 3; k++)
+            d[k] = cam->position[k] -
+                   (cam->image_top_left[k] + cam->pixel_delta_x[k] * x + cam->pixel_delta_y[k] * i);
+        dmax = std::fmax(dmax, std::sqrt(dot3(d, d)));
+    }
+    if (!(dmax > 0) || !std::isfinite(dmax)) return;
+    boxes_for(ctx, P, dmax, cam->width, row0, nrows, p.box);
     p.nbox = np;
+    // mirror bins: the camera reflected in each wall's plane, shifted by the reference's
+    // 1e-4 * normal origin offset (main.cpp:111); rows of (R M)^-1 = R * rows of M^-1.
+    // Reflected directions are unit vectors and d's are not: |R d| = |d| keeps dmax.
+    if (ctx->nW * np > rt::MIR_MAX_BOXES) return;
+    for (int w = 0; w < ctx->nW; w++) {
+        const double* Wd = &ctx->h_wal[14 * w];
+        const double *Pw = Wd, *n = Wd + 3;
+        Proj M;
+        const double op[3] = {P.o[0] - Pw[0], P.o[1] - Pw[1], P.o[2] - Pw[2]};
+        const double h = dot3(op, n);
+        for (int k = 0; k < 3; k++) M.o[k] = (P.o[k] - 2 * h * n[k]) + 1e-4 * n[k];
+        for (int j = 0; j < 3; j++) {
+            const double rn = dot3(P.r[j], n);
+            for (int k = 0; k < 3; k++) M.r[j][k] = P.r[j][k] - 2 * rn * n[k];
+        }
+        boxes_for(ctx, M, dmax, cam->width, row0, nrows, p.mbox + w * np);
+    }
+    p.nmir = ctx->nW;
 }
 
 rt::KParams make_params(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nrows,

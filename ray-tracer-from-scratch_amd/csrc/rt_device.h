@@ -94,6 +94,13 @@ constexpr int EYE_MAX_W = 16;
 // missed by the exact ray by an angle ~1e12 times the reference's rounding, so the
 // reference's own test rejects it too.  Scenes of <= 64 primitives.
 constexpr int BIN_MAX_PRIMS = 64;
+// Mirror bins.  A reflection off a plane is linear: the first-bounce ray of pixel (x, i)
+// off wall w (origin pos + 1e-4 n, direction reflect(d, n), main.cpp:111-113) lies on the
+// line from the camera mirrored in w's plane (shifted by 1e-4 n) with direction R d(x, i),
+// R = I - 2 n n^T, again affine in (x, i).  So a wave whose live rays all hit the same
+// wall can cull its first bounce with per-pixel boxes of a virtual camera, computed per
+// frame for every wall like the primary boxes.
+constexpr int MIR_MAX_BOXES = 128;
 struct PrimBox {
     int16_t x0, x1, i0, i1;  // inclusive pixel box (frame rows); x0 > x1 = never hit
 };
@@ -120,6 +127,10 @@ struct KParams {
     int32_t nbox;               // primitives with a PrimBox (nS + nW), 0 = tile bins off
     int32_t pad_box;
     PrimBox box[BIN_MAX_PRIMS]; // material-slot order: spheres, then walls
+    int32_t nmir;               // walls with mirror boxes (0 or nW)
+    int32_t pad_mir;
+    PrimBox mbox[MIR_MAX_BOXES];  // [wall w][slot j]: primitive j through the camera
+                                  // mirrored in wall w (first bounce), nmir * nbox used
     int32_t eye;                        // eye tables below valid
     int32_t pad_eye;
     double eye_s[EYE_MAX_S][4];         // sphere s: {oc.x, oc.y, oc.z, |oc|^2 - r^2}

@@ -680,24 +680,38 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
 }
 /* The primitives whose pixel box meets this wave's 8x8 tile (rt_device.h PrimBox): lane l
  * tests box l, one ballot.  Call with every lane active. */
-__device__ __forceinline__ uint64_t tile_keep(const KParams& p) {
+__device__ __forceinline__ uint64_t tile_keep(const KParams& p, const PrimBox* boxes) {
     const int wave = threadIdx.x >> 6;
     const int tx0 = blockIdx.x * TILE_W + (TILE_W > 8 ? (wave & 1) * 8 : 0);
     const int ty0 = p.row0 + blockIdx.y * TILE_H + (TILE_H > 8 ? (wave >> 1) * 8 : 0);
     const int l = threadIdx.x & 63;
     bool hit = false;
     if (l < p.nbox) {
-        const PrimBox b = p.box[l];
+        const PrimBox b = boxes[l];
         hit = b.x0 <= tx0 + 7 && b.x1 >= tx0 && b.i0 <= ty0 + 7 && b.i1 >= ty0;
     }
     return uniform64(__ballot(hit));
+}
+__device__ __forceinline__ uint64_t tile_keep(const KParams& p) { return tile_keep(p, p.box); }
+
+/* First bounce off one wall (rt_device.h "mirror bins"): when every live lane's primary
+ * ray hit the same wall w, the wave's reflected rays are primary rays of the virtual
+ * camera mirrored in w, whose per-primitive pixel boxes the host provides.  Returns the
+ * keep mask, or ~0 when the lanes' walls differ (or a sphere was hit).  prev: the material
+ * slot the lane's previous segment hit (valid where alive).  All lanes active. */
+__device__ __forceinline__ uint64_t mirror_keep(const KParams& p, bool alive, int prev) {
+    const uint64_t live = uniform64(__ballot(alive));
+    if (live == 0) return ~0ull;
+    const int slot0 = __builtin_amdgcn_readlane(prev, __builtin_ctzll(live));
+    if (slot0 < p.nS || uniform64(__ballot(alive && prev != slot0)) != 0) return ~0ull;
+    return tile_keep(p, p.mbox + (slot0 - p.nS) * p.nbox);
 }
 
 /* find_closest_hit for one segment of every live lane: the wave-culled scan (CULL) or the
  * linear scan.  Converged: every lane of the wave calls it (alive masks the tests). */
 template <bool MIXED, bool CULL>
 __device__ __forceinline__ HitD scan_d(const KParams& p, const RayD& r, bool alive,
-                                       bool primary, uint64_t keep) {
+                                       bool primary, bool binned, uint64_t keep) {
     HitD h = no_hit();
     if (CULL) {
         // walls first: their distances then bound the sphere tests
@@ -733,9 +747,9 @@ __device__ __forceinline__ HitD scan_d(const KParams& p, const RayD& r, bool ali
     } else if (alive) {
         // primary, p.eye and p.bins are wave-uniform: one scan or another per wave (MIXED
         // keeps its fp32 cull in front of every test: no eye tables, A/B +1.5%)
-        if (primary && p.nbox > 0) {
-            h = (!MIXED && p.eye) ? closest_hit_bin<MIXED, true>(p, r, keep)
-                                  : closest_hit_bin<MIXED, false>(p, r, keep);
+        if (binned) {
+            h = (!MIXED && primary && p.eye) ? closest_hit_bin<MIXED, true>(p, r, keep)
+                                             : closest_hit_bin<MIXED, false>(p, r, keep);
         } else {
             h = (!MIXED && primary && p.eye) ? closest_hit_d<MIXED, true>(p, r)
                                              : closest_hit_d<MIXED, false>(p, r);
@@ -766,7 +780,12 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
     // reduce over its live rays; k is wave-uniform.
     for (int k = 0;; ++k) {
         if (!__any(alive)) break;
-        const HitD h = scan_d<MIXED, CULL>(p, r, alive, k == 0, keep);
+        // tile bins: the primary segment, and the first bounce when the whole wave
+        // reflected off one wall (both wave-uniform)
+        uint64_t km = ~0ull;
+        if (!CULL && k == 0 && p.nbox > 0) km = keep;
+        if (!CULL && k == 1 && p.nmir > 0) km = mirror_keep(p, alive, st_m[0]);
+        const HitD h = scan_d<MIXED, CULL>(p, r, alive, k == 0, km != ~0ull, km);
         if (!alive) continue;
         ++segs;
         const bool last = k >= p.depth || k >= MAXD;  // remaining_iterations <= 0 (main.cpp:105)

@@ -411,11 +411,14 @@ def test_tile_bins_are_output_invariant(rend, prec):
     reference's own test rejects for every ray of a tile, and bounds tests it passes:
     frames with and without them are bitwise identical — random scenes and views, walls
     through the camera and seen edge-on, wide and narrow fields of view, ragged images,
-    row bands, up to the 64-primitive limit."""
+    row bands, up to the 64-primitive limit; the mirror bins of the first bounce off a wall
+    (camera reflected in the wall's plane) likewise."""
     rng = np.random.default_rng(31)
     rend.set_option(capi.RT_OPT_WAVE_CULL_MIN_SPHERES, 2**31 - 1)  # linear scan up to 64 prims
     try:
-        trials = [(1, 0), (0, 1), (5, 3), (8, 4), (8, 6), (20, 12), (40, 24), (58, 6), (3, 40)]
+        # <= 128 wall x primitive pairs also exercise the mirror (first-bounce) bins
+        trials = [(1, 0), (0, 1), (5, 3), (8, 4), (8, 6), (2, 9), (0, 11), (4, 7), (20, 12),
+                  (40, 24), (58, 6), (3, 40)]
         for trial, (ns, nw) in enumerate(trials * 2):
             sc = scenes.synthetic_scene(ns, min(nw, 6), seed=int(rng.integers(1 << 30)))
             pos = rng.uniform([-1, -3, -1], [5, 3, 2])
