@@ -141,10 +141,14 @@ enum rt_option {
     RT_OPT_EYE_TABLES = 3,            /* 1 (default): primary rays use per-frame tables of
                                          their camera-origin terms (small scenes); 0 = off.
                                          Output is identical. */
-    RT_OPT_TILE_BINS = 4              /* 1 (default): a per-frame pre-pass proves, per 8x8
-                                         tile, which primitives no primary ray of the tile
-                                         can hit (scenes of <= 64 primitives, exact
-                                         precisions); 0 = off.  Output is identical. */
+    RT_OPT_TILE_BINS = 4,             /* 1 (default): per-frame pixel boxes of every
+                                         primitive let each 8x8 tile test only what its
+                                         primary rays (and first bounce off one wall) can
+                                         hit (scenes of <= 64 primitives); 0 = off.
+                                         Output is identical. */
+    RT_OPT_ROW_ORDER = 5              /* 1 (default): tile rows are dispatched centre-out
+                                         from the estimated heaviest row (scheduling only);
+                                         0 = top to bottom.  Output is identical. */
 };
 int rt_set_option(rt_ctx* ctx, int32_t option, int64_t value);
 

@@ -7,6 +7,7 @@
  */
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -29,6 +30,8 @@ struct rt_ctx {
     int wave_cull_min = 24;  // spheres from which the wave cull pays (tools/sweep.py)
     bool eye_tables = true;  // RT_OPT_EYE_TABLES
     bool tile_bins = true;   // RT_OPT_TILE_BINS
+    bool row_order = true;   // RT_OPT_ROW_ORDER
+    std::vector<double> h_km;   // metallic of each material slot
     size_t off_s64 = 0, off_w32 = 0, off_w64 = 0, off_sj = 0, off_wj = 0, off_mat = 0, off_mat32 = 0;
     void* d_out = nullptr;
     size_t d_out_cap = 0;
@@ -262,6 +265,30 @@ void frame_boxes(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t 
     if (!(dmax > 0) || !std::isfinite(dmax)) return;
     boxes_for(ctx, P, dmax, cam->width, row0, nrows, p.box);
     p.nbox = np;
+    // dispatch order (rt_trace.hip tile_row): centre-out from the weighted median tile row
+    // of the boxes' coverage, reflective primitives weighted up (their tiles bounce)
+    if (ctx->row_order) {
+        const int nty = (nrows + 7) / 8;
+        std::vector<double> prof(nty, 0.0);
+        for (int j = 0; j < np; j++) {
+            const rt::PrimBox& b = p.box[j];
+            const int x0 = std::max<int>(b.x0, 0), x1 = std::min<int>(b.x1, cam->width - 1);
+            const int i0 = std::max<int>(b.i0, row0), i1 = std::min<int>(b.i1, row0 + nrows - 1);
+            if (x0 > x1 || i0 > i1) continue;
+            const double wgt = (1.0 + 3.0 * ctx->h_km[j]) * (x1 - x0 + 1);
+            for (int t = (i0 - row0) / 8; t <= (i1 - row0) / 8; t++) prof[t] += wgt;
+        }
+        double tot = 0;
+        for (double v : prof) tot += v;
+        double acc = 0;
+        for (int t = 0; t < nty && tot > 0; t++) {
+            acc += prof[t];
+            if (acc >= 0.5 * tot) {
+                p.row_center = t;
+                break;
+            }
+        }
+    }
     // mirror bins: the camera reflected in each wall's plane, shifted by the reference's
     // 1e-4 * normal origin offset (main.cpp:111); rows of (R M)^-1 = R * rows of M^-1.
     // Reflected directions are unit vectors and d's are not: |R d| = |d| keeps dmax.
@@ -569,6 +596,8 @@ int rt_set_scene(rt_ctx* ctx, const rt_prim* prims, int32_t n) {
         const double e = mat[k].ex;
         if (!(e >= 0.0 && e <= 1024.0 && e == std::floor(e))) ctx->int_exp = false;
     }
+    ctx->h_km.assign(nS + nW, 0.0);
+    for (size_t k = 0; k < nS + nW; k++) ctx->h_km[k] = mat[k].km;
     ctx->h_sph.assign(5 * nS, 0.0);
     for (size_t s = 0; s < nS; s++) {
         for (int k = 0; k < 4; k++) ctx->h_sph[5 * s + k] = s64[s / 4].v[s % 4][k];
@@ -613,6 +642,10 @@ int rt_set_option(rt_ctx* ctx, int32_t option, int64_t value) {
         case RT_OPT_TILE_BINS:
             if (value != 0 && value != 1) return RT_ERR_INVALID_ARG;
             ctx->tile_bins = value == 1;
+            return RT_OK;
+        case RT_OPT_ROW_ORDER:
+            if (value != 0 && value != 1) return RT_ERR_INVALID_ARG;
+            ctx->row_order = value == 1;
             return RT_OK;
         default:
             return RT_ERR_INVALID_ARG;

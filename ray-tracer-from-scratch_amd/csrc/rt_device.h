@@ -125,7 +125,7 @@ struct KParams {
     unsigned long long* segs;   // may be null
     unsigned long long* stats;  // diagnostic counters, may be null (rt_set_option)
     int32_t nbox;               // primitives with a PrimBox (nS + nW), 0 = tile bins off
-    int32_t pad_box;
+    int32_t row_center;         // tile row dispatched first (rt_trace.hip tile_row), -1 = off
     PrimBox box[BIN_MAX_PRIMS]; // material-slot order: spheres, then walls
     int32_t nmir;               // walls with mirror boxes (0 or nW)
     int32_t pad_mir;

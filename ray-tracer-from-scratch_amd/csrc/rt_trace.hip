@@ -56,6 +56,9 @@
 #ifndef RT_TERMINAL_F32    // PATH64: the last segment of a path (sky, or the hit at max
 #define RT_TERMINAL_F32 1  // depth) feeds colour only, so its normalisations run in fp32
 #endif
+#ifndef RT_WAVE_TIMES      // diagnostic build: per-wave start/end stamps into KParams::stats
+#define RT_WAVE_TIMES 0    // (tools/wave_times.py); never on in the product
+#endif
 #ifndef RT_DIAG            // diagnostic build: count wave/lane entries of branch bodies
 #define RT_DIAG 0          // into g_diag (rt_diag_read); never on in the product
 #endif
@@ -209,6 +212,19 @@ constexpr int MAXD_SMALL = 4;
 constexpr int MAXD_MID = 8;
 constexpr int MAXD_REF = 10;  // rt_scene's default recursion depth (main.cpp:89)
 constexpr int MAXD_LARGE = 16;
+
+/* Waves deep into their paths are the kernel's critical path (its tail): from the
+ * RT_PRIO_FROM-th bounce on, a wave asks the sequencer for a higher issue priority. */
+#ifndef RT_PRIO_FROM
+#define RT_PRIO_FROM 0   // 0 = off
+#endif
+__device__ __forceinline__ void bounce_priority(int k) {
+    if (RT_PRIO_FROM > 0) {
+        if (k == RT_PRIO_FROM) __builtin_amdgcn_s_setprio(1);
+        if (k == RT_PRIO_FROM + 1) __builtin_amdgcn_s_setprio(2);
+        if (k == RT_PRIO_FROM + 2) __builtin_amdgcn_s_setprio(3);
+    }
+}
 
 /* ------------------------------------------------------------------------ */
 /* closest hit (find_closest_hit, main.cpp:67-84)                            */
@@ -673,6 +689,24 @@ __device__ __forceinline__ f3 local_color_f(const DevMat32& m, float s, float ks
 }
 __device__ __forceinline__ f3 tof(d3 v) { return F3((float)v.x, (float)v.y, (float)v.z); }
 
+/* Dispatch order of tile rows (workgroup row blockIdx.y -> tile row).  Per-tile cost is
+ * very uneven (sky/ground tiles end after one segment, tiles over reflective walls bounce
+ * to full depth), and a heavy wave dispatched late ends the kernel long after the last
+ * light one: the dispatcher goes row by row, so rows are visited centre-out from the
+ * host's estimate of the heaviest row (KParams::row_center, rt_capi.cpp) — heavy work
+ * first, the cheap rows fill in around it.  Identity when row_center < 0. */
+__device__ __forceinline__ int tile_row(const KParams& p) {
+    const int j = blockIdx.y, c = p.row_center, n = gridDim.y;
+    if (c < 0 || c >= n) return j;
+    const int L = min(c, n - 1 - c);  // rows c-L .. c+L alternate
+    if (j <= 2 * L) {
+        const int d = (j + 1) >> 1;
+        return (j & 1) ? c + d : c - d;
+    }
+    const int e = j - 2 * L;  // one side is exhausted: continue on the other
+    return (c - L == 0) ? c + L + e : c - L - e;
+}
+
 __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
     const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
     const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
@@ -683,7 +717,7 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
 __device__ __forceinline__ uint64_t tile_keep(const KParams& p, const PrimBox* boxes) {
     const int wave = threadIdx.x >> 6;
     const int tx0 = blockIdx.x * TILE_W + (TILE_W > 8 ? (wave & 1) * 8 : 0);
-    const int ty0 = p.row0 + blockIdx.y * TILE_H + (TILE_H > 8 ? (wave >> 1) * 8 : 0);
+    const int ty0 = p.row0 + tile_row(p) * TILE_H + (TILE_H > 8 ? (wave >> 1) * 8 : 0);
     const int l = threadIdx.x & 63;
     bool hit = false;
     if (l < p.nbox) {
@@ -780,6 +814,7 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
     // reduce over its live rays; k is wave-uniform.
     for (int k = 0;; ++k) {
         if (!__any(alive)) break;
+        bounce_priority(k);
         // tile bins: the primary segment, and the first bounce when the whole wave
         // reflected off one wall (both wave-uniform)
         uint64_t km = ~0ull;
@@ -990,15 +1025,22 @@ __device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, bool
     const uint64_t keep = (!CULL && p.nbox > 0) ? tile_keep(p) : ~0ull;  // all lanes active
     for (int k = 0;; ++k) {
         if (!__any(alive)) break;
+        bounce_priority(k);
         const float a = fdot(d, d);
         const float ra = frcp(a);
         const float rl = frsq(a);
         float best = FLT_MAX, bpt = 0.0f;
         int slot = -1;
-        if (!CULL && k == 0 && p.nbox > 0) {
-            // primary segment behind the tile bins: kept spheres in index order, kept walls
+        // tile bins: the primary segment, and the first bounce when the whole wave
+        // reflected off one wall (both wave-uniform)
+        uint64_t km = ~0ull;
+        if (!CULL && k == 0 && p.nbox > 0) km = keep;
+        if (!CULL && k == 1 && p.nmir > 0) km = mirror_keep(p, alive, st_m[0]);
+        const bool binned = km != ~0ull;
+        if (!CULL && binned) {
+            // kept spheres in index order, kept walls
             if (alive) {
-                uint64_t sm = p.nS >= 64 ? keep : keep & ((1ull << p.nS) - 1);
+                uint64_t sm = p.nS >= 64 ? km : km & ((1ull << p.nS) - 1);
                 while (sm) {
                     const int s = __builtin_ctzll(sm);
                     sm &= sm - 1;
@@ -1006,7 +1048,7 @@ __device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, bool
                     const float Sf[4] = {G.c[0][s & 3], G.c[1][s & 3], G.c[2][s & 3], G.c[3][s & 3]};
                     sphere_f(Sf, s, o, d, a, ra, rl, best, bpt, slot);
                 }
-                walls_f(p, o, d, best, slot, p.nS >= 64 ? 0 : keep >> p.nS);
+                walls_f(p, o, d, best, slot, p.nS >= 64 ? 0 : km >> p.nS);
             }
         } else if (CULL) {
             if (RT_WALLS_FIRST && alive) walls_f(p, o, d, best, slot);
@@ -1053,7 +1095,7 @@ __device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, bool
         }
         if (!alive) continue;
         ++segs;
-        if (!CULL && !(k == 0 && p.nbox > 0)) walls_f(p, o, d, best, slot);
+        if (!CULL && !binned) walls_f(p, o, d, best, slot);
         const f3 nv = d * rl;
         if (slot < 0) {
             if (d.z < 0.0f) {
@@ -1167,10 +1209,13 @@ template <int PREC, bool SUN, bool INT_EXP, bool CULL, int MAXD>
 __global__ void __launch_bounds__(BLOCK)
 __attribute__((amdgpu_waves_per_eu(waves_per_eu<PREC, SUN, INT_EXP, CULL, MAXD>(), 8)))
 k_trace(KParams p) {
+#if RT_WAVE_TIMES
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+#endif
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int x = blockIdx.x * TILE_W + (TILE_W > 8 ? (wave & 1) * 8 : 0) + (lane & 7);
-    const int r = blockIdx.y * TILE_H + (TILE_H > 8 ? (wave >> 1) * 8 : 0) + (lane >> 3);
+    const int r = tile_row(p) * TILE_H + (TILE_H > 8 ? (wave >> 1) * 8 : 0) + (lane >> 3);
     const bool valid = x < p.W && r < p.nrows;
     const int i = p.row0 + r;
     int segs = 0;
@@ -1185,6 +1230,16 @@ k_trace(KParams p) {
         if (valid) store_pixel(p, r, x, c.x, c.y, c.z);
     }
     count_segments(p, segs);
+#if RT_WAVE_TIMES
+    // diagnostic build: per wave {start, end, segments << 32 | CU id} (100 MHz clock)
+    for (int off = 32; off > 0; off >>= 1) segs += __shfl_xor(segs, off, 64);
+    if (p.stats != nullptr && lane == 0) {
+        const size_t wid = ((size_t)tile_row(p) * gridDim.x + blockIdx.x) * (BLOCK / 64) + wave;
+        p.stats[3 * wid] = t_start;
+        p.stats[3 * wid + 1] = __builtin_amdgcn_s_memrealtime();
+        p.stats[3 * wid + 2] = ((unsigned long long)segs << 32) | (unsigned)__smid();
+    }
+#endif
 }
 
 template <int PREC, bool SUN, bool INT_EXP, bool CULL>

@@ -47,6 +47,7 @@ RT_OPT_WAVE_CULL_MIN_SPHERES = 1
 RT_OPT_STATS_DEVICE_PTR = 2
 RT_OPT_EYE_TABLES = 3
 RT_OPT_TILE_BINS = 4
+RT_OPT_ROW_ORDER = 5
 
 
 class rt_material(C.Structure):

@@ -451,6 +451,26 @@ def test_tile_bins_are_output_invariant(rend, prec):
         rend.set_option(capi.RT_OPT_WAVE_CULL_MIN_SPHERES, 24)
 
 
+def test_row_order_is_output_invariant(rend):
+    """Centre-out tile-row dispatch (RT_OPT_ROW_ORDER) only reorders work: bitwise equal
+    frames and segment counts, on full frames and row bands of ragged sizes."""
+    sc = scenes.synthetic_scene(8, 4)
+    rend.set_scene(scenes.to_prims(sc))
+    try:
+        for w, h, r0, n in ((160, 90, 0, 90), (203, 117, 13, 71), (64, 36, 35, 1)):
+            cam = capi.camera_init(**scenes.camera_args(w, h))
+            imgs = []
+            for on in (1, 0):
+                rend.set_option(capi.RT_OPT_ROW_ORDER, on)
+                img, st = rend.render(cam, 4, capi.RT_PREC_PATH64, 0, capi.RT_OUT_RGB_F32,
+                                      count_segments=True, row0=r0, nrows=n)
+                imgs.append((img, st.segments))
+            assert imgs[0][1] == imgs[1][1]
+            assert np.array_equal(imgs[0][0].view(np.uint32), imgs[1][0].view(np.uint32))
+    finally:
+        rend.set_option(capi.RT_OPT_ROW_ORDER, 1)
+
+
 # ---------------------------------------------------------------- multi-GPU path (1 rank)
 def test_render_tiled_rccl_single_rank(rend):
     """rtamd.tiling.render_tiled over the nccl (RCCL) backend with one rank: the gathered
