@@ -143,12 +143,16 @@ enum rt_option {
                                          Output is identical. */
     RT_OPT_TILE_BINS = 4,             /* 1 (default): per-frame pixel boxes of every
                                          primitive let each 8x8 tile test only what its
-                                         primary rays (and first bounce off one wall) can
-                                         hit (scenes of <= 64 primitives); 0 = off.
+                                         primary rays can hit (scenes of <= 64
+                                         primitives); 0 = off.
                                          Output is identical. */
-    RT_OPT_ROW_ORDER = 5              /* 1 (default): tile rows are dispatched centre-out
+    RT_OPT_ROW_ORDER = 5,             /* 1 (default): tile rows are dispatched centre-out
                                          from the estimated heaviest row (scheduling only);
                                          0 = top to bottom.  Output is identical. */
+    RT_OPT_MIRROR_BINS = 6            /* 1 (default): bounces that follow the same wall
+                                         chain across a wave use the boxes of the mirrored
+                                         camera (needs RT_OPT_TILE_BINS); 0 = off.  Output
+                                         is identical. */
 };
 int rt_set_option(rt_ctx* ctx, int32_t option, int64_t value);
 

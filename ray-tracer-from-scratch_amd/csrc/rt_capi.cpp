@@ -31,6 +31,7 @@ struct rt_ctx {
     bool eye_tables = true;  // RT_OPT_EYE_TABLES
     bool tile_bins = true;   // RT_OPT_TILE_BINS
     bool row_order = true;   // RT_OPT_ROW_ORDER
+    bool mirror_bins = true; // RT_OPT_MIRROR_BINS
     std::vector<double> h_km;   // metallic of each material slot
     size_t off_s64 = 0, off_w32 = 0, off_w64 = 0, off_sj = 0, off_wj = 0, off_mat = 0, off_mat32 = 0;
     void* d_out = nullptr;
@@ -245,7 +246,7 @@ void boxes_for(const rt_ctx* ctx, const Proj& P, double dmax, int32_t width, int
 void frame_boxes(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nrows,
                  rt::KParams& p) {
     p.nbox = 0;
-    p.nmir = 0;
+    p.mir_depth = 0;
     const int np = ctx->nS + ctx->nW;
     if (!ctx->tile_bins || p.wave_cull || np == 0 || np > rt::BIN_MAX_PRIMS || cam->width > 32000 ||
         cam->height > 32000 || nrows <= 0 || cam->width <= 0)
@@ -289,24 +290,77 @@ void frame_boxes(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t 
             }
         }
     }
-    // mirror bins: the camera reflected in each wall's plane, shifted by the reference's
-    // 1e-4 * normal origin offset (main.cpp:111); rows of (R M)^-1 = R * rows of M^-1.
-    // Reflected directions are unit vectors and d's are not: |R d| = |d| keeps dmax.
-    if (ctx->nW * np > rt::MIR_MAX_BOXES) return;
-    for (int w = 0; w < ctx->nW; w++) {
-        const double* Wd = &ctx->h_wal[14 * w];
-        const double *Pw = Wd, *n = Wd + 3;
-        Proj M;
-        const double op[3] = {P.o[0] - Pw[0], P.o[1] - Pw[1], P.o[2] - Pw[2]};
-        const double h = dot3(op, n);
-        for (int k = 0; k < 3; k++) M.o[k] = (P.o[k] - 2 * h * n[k]) + 1e-4 * n[k];
-        for (int j = 0; j < 3; j++) {
-            const double rn = dot3(P.r[j], n);
-            for (int k = 0; k < 3; k++) M.r[j][k] = P.r[j][k] - 2 * rn * n[k];
-        }
-        boxes_for(ctx, M, dmax, cam->width, row0, nrows, p.mbox + w * np);
+    // mirror bins (rt_device.h): cameras mirrored along wall chains, each reflection
+    // shifted by the reference's 1e-4 * normal origin offset (main.cpp:111); rows of
+    // (R M)^-1 = R * rows of M^-1.  Reflected directions are unit vectors, not the d's,
+    // but |R d| = |d| keeps dmax.  Only chains some tile can follow are computed (their
+    // "reach" — the intersection of the boxes along the chain, widened by a tile — is
+    // non-empty); every other sequence keeps all primitives.
+    const int nW = ctx->nW;
+    int depth = 0;
+    for (long tot = 0, lvl = 1; depth < rt::MIR_MAX_DEPTH && nW > 0; depth++) {
+        lvl *= nW;
+        tot += lvl * np;
+        if (tot > rt::MIR_MAX_BOXES) break;
     }
-    p.nmir = ctx->nW;
+    if (!ctx->mirror_bins || depth == 0) return;
+    struct Node {
+        Proj cam;
+        rt::PrimBox reach;  // pixel region (incl. a tile of slack) where the chain can occur
+    };
+    const rt::PrimBox allb{-1, (int16_t)cam->width, (int16_t)(row0 - 1), (int16_t)(row0 + nrows)};
+    auto meet = [](const rt::PrimBox& a, const rt::PrimBox& b) {
+        rt::PrimBox r{std::max(a.x0, b.x0), std::min(a.x1, b.x1), std::max(a.i0, b.i0),
+                      std::min(a.i1, b.i1)};
+        return r;
+    };
+    auto empty = [](const rt::PrimBox& b) { return b.x0 > b.x1 || b.i0 > b.i1; };
+    auto widen = [](rt::PrimBox b) {
+        if (b.x0 > b.x1 || b.i0 > b.i1) return b;
+        b.x0 = (int16_t)(b.x0 - 8);
+        b.x1 = (int16_t)(b.x1 + 8);
+        b.i0 = (int16_t)(b.i0 - 8);
+        b.i1 = (int16_t)(b.i1 + 8);
+        return b;
+    };
+    std::vector<Node> prev(1), cur;  // level 0: the camera itself, reach = the frame
+    prev[0].cam = P;
+    prev[0].reach = allb;
+    std::vector<const rt::PrimBox*> prev_boxes(1, p.box);
+    int off = 0;
+    for (int L = 1; L <= depth; L++) {
+        cur.assign(prev.size() * nW, Node{});
+        std::vector<const rt::PrimBox*> cur_boxes(cur.size(), nullptr);
+        for (size_t q0 = 0; q0 < prev.size(); q0++) {
+            for (int w = 0; w < nW; w++) {
+                const size_t q = q0 * nW + w;
+                rt::PrimBox* out = p.mbox + (size_t)(off + q) * np;
+                Node& nd = cur[q];
+                nd.reach = empty(prev[q0].reach) ? prev[q0].reach
+                                                 : meet(prev[q0].reach, widen(prev_boxes[q0][ctx->nS + w]));
+                if (empty(nd.reach)) {
+                    for (int j = 0; j < np; j++) out[j] = allb;  // never followed: keep all
+                    continue;
+                }
+                const double* Wd = &ctx->h_wal[14 * w];
+                const double *Pw = Wd, *n = Wd + 3;
+                const Proj& pc = prev[q0].cam;
+                const double op[3] = {pc.o[0] - Pw[0], pc.o[1] - Pw[1], pc.o[2] - Pw[2]};
+                const double h = dot3(op, n);
+                for (int k = 0; k < 3; k++) nd.cam.o[k] = (pc.o[k] - 2 * h * n[k]) + 1e-4 * n[k];
+                for (int j = 0; j < 3; j++) {
+                    const double rn = dot3(pc.r[j], n);
+                    for (int k = 0; k < 3; k++) nd.cam.r[j][k] = pc.r[j][k] - 2 * rn * n[k];
+                }
+                boxes_for(ctx, nd.cam, dmax, cam->width, row0, nrows, out);
+                cur_boxes[q] = out;
+            }
+        }
+        off += (int)cur.size();
+        prev.swap(cur);
+        prev_boxes.swap(cur_boxes);
+    }
+    p.mir_depth = depth;
 }
 
 rt::KParams make_params(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nrows,
@@ -642,6 +696,10 @@ int rt_set_option(rt_ctx* ctx, int32_t option, int64_t value) {
         case RT_OPT_TILE_BINS:
             if (value != 0 && value != 1) return RT_ERR_INVALID_ARG;
             ctx->tile_bins = value == 1;
+            return RT_OK;
+        case RT_OPT_MIRROR_BINS:
+            if (value != 0 && value != 1) return RT_ERR_INVALID_ARG;
+            ctx->mirror_bins = value == 1;
             return RT_OK;
         case RT_OPT_ROW_ORDER:
             if (value != 0 && value != 1) return RT_ERR_INVALID_ARG;

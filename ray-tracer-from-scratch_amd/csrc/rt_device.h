@@ -97,10 +97,14 @@ constexpr int BIN_MAX_PRIMS = 64;
 // Mirror bins.  A reflection off a plane is linear: the first-bounce ray of pixel (x, i)
 // off wall w (origin pos + 1e-4 n, direction reflect(d, n), main.cpp:111-113) lies on the
 // line from the camera mirrored in w's plane (shifted by 1e-4 n) with direction R d(x, i),
-// R = I - 2 n n^T, again affine in (x, i).  So a wave whose live rays all hit the same
-// wall can cull its first bounce with per-pixel boxes of a virtual camera, computed per
-// frame for every wall like the primary boxes.
-constexpr int MIR_MAX_BOXES = 128;
+// R = I - 2 n n^T, again affine in (x, i); a chain of wall bounces composes the
+// reflections.  So a wave whose live rays all followed the same wall sequence can cull
+// the next segment with the pixel boxes of that virtual camera, computed per frame like
+// the primary boxes for every sequence of up to MIR_MAX_DEPTH walls that some tile can
+// follow.  Sequence (w1..wL) of level L: boxes at mbox[(off_L + q) * nbox ..], q the
+// base-nW number w1..wL, off_L = nW + nW^2 + .. + nW^(L-1).
+constexpr int MIR_MAX_DEPTH = 3;
+constexpr int MIR_MAX_BOXES = 1024;
 struct PrimBox {
     int16_t x0, x1, i0, i1;  // inclusive pixel box (frame rows); x0 > x1 = never hit
 };
@@ -127,10 +131,10 @@ struct KParams {
     int32_t nbox;               // primitives with a PrimBox (nS + nW), 0 = tile bins off
     int32_t row_center;         // tile row dispatched first (rt_trace.hip tile_row), -1 = off
     PrimBox box[BIN_MAX_PRIMS]; // material-slot order: spheres, then walls
-    int32_t nmir;               // walls with mirror boxes (0 or nW)
+    int32_t mir_depth;          // wall-sequence levels with mirror boxes (0 = off)
     int32_t pad_mir;
-    PrimBox mbox[MIR_MAX_BOXES];  // [wall w][slot j]: primitive j through the camera
-                                  // mirrored in wall w (first bounce), nmir * nbox used
+    PrimBox mbox[MIR_MAX_BOXES];  // [sequence][slot j]: primitive j through the camera
+                                  // mirrored along the sequence (see above)
     int32_t eye;                        // eye tables below valid
     int32_t pad_eye;
     double eye_s[EYE_MAX_S][4];         // sphere s: {oc.x, oc.y, oc.z, |oc|^2 - r^2}

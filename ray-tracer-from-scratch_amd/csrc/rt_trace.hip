@@ -728,17 +728,30 @@ __device__ __forceinline__ uint64_t tile_keep(const KParams& p, const PrimBox* b
 }
 __device__ __forceinline__ uint64_t tile_keep(const KParams& p) { return tile_keep(p, p.box); }
 
-/* First bounce off one wall (rt_device.h "mirror bins"): when every live lane's primary
- * ray hit the same wall w, the wave's reflected rays are primary rays of the virtual
- * camera mirrored in w, whose per-primitive pixel boxes the host provides.  Returns the
- * keep mask, or ~0 when the lanes' walls differ (or a sphere was hit).  prev: the material
- * slot the lane's previous segment hit (valid where alive).  All lanes active. */
-__device__ __forceinline__ uint64_t mirror_keep(const KParams& p, bool alive, int prev) {
+/* Bounce k <= mir_depth after a chain of wall hits (rt_device.h "mirror bins"): when
+ * every live lane's previous k segments hit the same walls in the same order, the wave's
+ * rays are primary rays of the camera mirrored along that chain, whose per-primitive
+ * pixel boxes the host provides.  Returns the keep mask, or ~0 when the lanes' paths
+ * differ (or a sphere was hit).  st_m: the lane's material-slot stack (valid where
+ * alive).  All lanes active; k wave-uniform. */
+template <int MAXD>
+__device__ __forceinline__ uint64_t mirror_keep(const KParams& p, bool alive, const int* st_m,
+                                                int k) {
     const uint64_t live = uniform64(__ballot(alive));
-    if (live == 0) return ~0ull;
-    const int slot0 = __builtin_amdgcn_readlane(prev, __builtin_ctzll(live));
-    if (slot0 < p.nS || uniform64(__ballot(alive && prev != slot0)) != 0) return ~0ull;
-    return tile_keep(p, p.mbox + (slot0 - p.nS) * p.nbox);
+    if (live == 0 || k > p.mir_depth) return ~0ull;
+    const int l0 = __builtin_ctzll(live);
+    int q = 0, off = 0, lvl = 1;
+#pragma unroll
+    for (int j = 0; j < MIR_MAX_DEPTH && j < MAXD; ++j) {
+        if (j < k) {
+            const int sj = __builtin_amdgcn_readlane(st_m[j], l0);
+            if (sj < p.nS || uniform64(__ballot(alive && st_m[j] != sj)) != 0) return ~0ull;
+            q = q * p.nW + (sj - p.nS);
+            if (j > 0) off += lvl;
+            lvl *= p.nW;
+        }
+    }
+    return tile_keep(p, p.mbox + (off + q) * p.nbox);
 }
 
 /* find_closest_hit for one segment of every live lane: the wave-culled scan (CULL) or the
@@ -819,7 +832,7 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
         // reflected off one wall (both wave-uniform)
         uint64_t km = ~0ull;
         if (!CULL && k == 0 && p.nbox > 0) km = keep;
-        if (!CULL && k == 1 && p.nmir > 0) km = mirror_keep(p, alive, st_m[0]);
+        if (!CULL && k >= 1 && k <= p.mir_depth) km = mirror_keep<MAXD>(p, alive, st_m, k);
         const HitD h = scan_d<MIXED, CULL>(p, r, alive, k == 0, km != ~0ull, km);
         if (!alive) continue;
         ++segs;
@@ -1035,7 +1048,7 @@ __device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, bool
         // reflected off one wall (both wave-uniform)
         uint64_t km = ~0ull;
         if (!CULL && k == 0 && p.nbox > 0) km = keep;
-        if (!CULL && k == 1 && p.nmir > 0) km = mirror_keep(p, alive, st_m[0]);
+        if (!CULL && k >= 1 && k <= p.mir_depth) km = mirror_keep<MAXD>(p, alive, st_m, k);
         const bool binned = km != ~0ull;
         if (!CULL && binned) {
             // kept spheres in index order, kept walls

@@ -48,6 +48,7 @@ RT_OPT_STATS_DEVICE_PTR = 2
 RT_OPT_EYE_TABLES = 3
 RT_OPT_TILE_BINS = 4
 RT_OPT_ROW_ORDER = 5
+RT_OPT_MIRROR_BINS = 6
 
 
 class rt_material(C.Structure):
