@@ -33,7 +33,8 @@ struct rt_ctx {
     bool row_order = true;   // RT_OPT_ROW_ORDER
     bool mirror_bins = true; // RT_OPT_MIRROR_BINS
     std::vector<double> h_km;   // metallic of each material slot
-    size_t off_s64 = 0, off_w32 = 0, off_w64 = 0, off_sj = 0, off_wj = 0, off_mat = 0, off_mat32 = 0;
+    size_t off_s64 = 0, off_w32 = 0, off_w64 = 0, off_sj = 0, off_wj = 0, off_mat = 0, off_mat32 = 0,
+           off_wnn = 0;
     void* d_out = nullptr;
     size_t d_out_cap = 0;
     unsigned long long* d_segs = nullptr;
@@ -376,6 +377,7 @@ rt::KParams make_params(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, i
     p.wall_j = reinterpret_cast<const int32_t*>(base + ctx->off_wj);
     p.mat = reinterpret_cast<const rt::DevMat*>(base + ctx->off_mat);
     p.mat32 = reinterpret_cast<const rt::DevMat32*>(base + ctx->off_mat32);
+    p.wnn = reinterpret_cast<const double(*)[4]>(base + ctx->off_wnn);
     p.nS = ctx->nS;
     p.nW = ctx->nW;
     p.int_exp = ctx->int_exp ? 1 : 0;
@@ -574,7 +576,8 @@ int rt_set_scene(rt_ctx* ctx, const rt_prim* prims, int32_t n) {
     const size_t off_wj = align_up(off_sj + nS * sizeof(int32_t), 256);
     const size_t off_mat = align_up(off_wj + nW * sizeof(int32_t), 256);
     const size_t off_mat32 = align_up(off_mat + (nS + nW) * sizeof(rt::DevMat), 256);
-    const size_t total = align_up(off_mat32 + (nS + nW) * sizeof(rt::DevMat32), 256) + 256;
+    const size_t off_wnn = align_up(off_mat32 + (nS + nW) * sizeof(rt::DevMat32), 256);
+    const size_t total = align_up(off_wnn + nW * 4 * sizeof(double), 256) + 256;
     std::vector<char> host(total, 0);
     auto* s32 = reinterpret_cast<rt::SphG32*>(host.data());
     auto* s64 = reinterpret_cast<rt::SphG64*>(host.data() + off_s64);
@@ -584,6 +587,7 @@ int rt_set_scene(rt_ctx* ctx, const rt_prim* prims, int32_t n) {
     auto* wj = reinterpret_cast<int32_t*>(host.data() + off_wj);
     auto* mat = reinterpret_cast<rt::DevMat*>(host.data() + off_mat);
     auto* mat32 = reinterpret_cast<rt::DevMat32*>(host.data() + off_mat32);
+    auto* wnn = reinterpret_cast<double(*)[4]>(host.data() + off_wnn);
     auto put_mat = [&](size_t slot, const rt_material& m) {
         rt::DevMat& d = mat[slot];
         for (int k = 0; k < 3; k++) d.color[k] = m.color[k];
@@ -630,6 +634,10 @@ int rt_set_scene(rt_ctx* ctx, const rt_prim* prims, int32_t n) {
         w32[w].wid = (float)a.wid;
         wj[w] = a.j;
         put_mat(nS + w, prims[a.j].mat);
+        const hv3 nn = hnormalize(hv3{a.n[0], a.n[1], a.n[2]});  // N.normalize(), vec.cpp:21
+        wnn[w][0] = nn.x;
+        wnn[w][1] = nn.y;
+        wnn[w][2] = nn.z;
     }
 
     RT_HIP(ctx, hipSetDevice(ctx->device));
@@ -675,6 +683,7 @@ int rt_set_scene(rt_ctx* ctx, const rt_prim* prims, int32_t n) {
     ctx->off_wj = off_wj;
     ctx->off_mat = off_mat;
     ctx->off_mat32 = off_mat32;
+    ctx->off_wnn = off_wnn;
     ctx->have_scene = true;
     return RT_OK;
 }

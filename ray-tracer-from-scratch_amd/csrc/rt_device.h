@@ -12,6 +12,7 @@
  *   int32  wall_j[nW]     scene index of each wall (tie-break only)
  *   DevMat [nS + nW]      64 B, spheres first then walls, indexed by "material slot"
  *   DevMat32 [nS + nW]    32 B, fp32 copy for the fp32 colour paths
+ *   double wnn[nW][4]     normalize(n) of each wall (32 B)
  *
  * The per-ray scan (find_closest_hit, main.cpp:67-84) runs one loop over sphere groups
  * and one over walls instead of a virtual call per primitive.  Every lane of a wave tests
@@ -118,6 +119,8 @@ struct KParams {
     const int32_t* wall_j;
     const DevMat* mat;     // [nS + nW]
     const DevMat32* mat32; // [nS + nW]
+    const double (*wnn)[4];  // [nW] normalize(wall normal) (vec.cpp:21, host), the normal
+                             // every reflection / shading step normalises again
     int32_t nS, nW;
     int32_t int_exp;       // every specular exponent is an integer in [0, 1024]
     int32_t wave_cull;     // cull spheres per wave (rt_trace.hip) before the per-lane tests

@@ -56,6 +56,12 @@
 #ifndef RT_TERMINAL_F32    // PATH64: the last segment of a path (sky, or the hit at max
 #define RT_TERMINAL_F32 1  // depth) feeds colour only, so its normalisations run in fp32
 #endif
+#ifndef RT_LAZY_TERMS      // PATH64: |d|^2, 1/|d|^2, |d| only when a sphere test or a
+#define RT_LAZY_TERMS 0    // reflection needs them (wave-uniform; A/B: +2% at c2, off)
+#endif
+#ifndef RT_BOX_SCHED_BARRIER
+#define RT_BOX_SCHED_BARRIER 1
+#endif
 #ifndef RT_WAVE_TIMES      // diagnostic build: per-wave start/end stamps into KParams::stats
 #define RT_WAVE_TIMES 0    // (tools/wave_times.py); never on in the product
 #endif
@@ -661,6 +667,21 @@ __device__ __forceinline__ RayD make_ray(d3 o, d3 d) {
     r.dlen = sqrt_e(r.a);
     return r;
 }
+/* Origin and direction only: |d|^2, its reciprocal and |d| are formed by ray_terms when a
+ * sphere test or a reflection needs them (wave-uniform decisions; walls and fp32 terminal
+ * shading use none of them). */
+__device__ __forceinline__ RayD make_ray_lazy(d3 o, d3 d) {
+    RayD r;
+    r.o = o;
+    r.d = d;
+    r.a = r.ra = r.dlen = 0.0;
+    return r;
+}
+__device__ __forceinline__ void ray_terms(RayD& r) {
+    r.a = lensq(r.d);
+    r.ra = rcp_refined(r.a);
+    r.dlen = sqrt_e(r.a);
+}
 
 /* fp32 shading of one hit for PATH64: the same formulas as shade_d on the exact fp64
  * geometry rounded to fp32 (colour only — nothing here feeds the next ray). */
@@ -713,20 +734,26 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
     return ((uint64_t)hi << 32) | lo;
 }
 /* The primitives whose pixel box meets this wave's 8x8 tile (rt_device.h PrimBox): lane l
- * tests box l, one ballot.  Call with every lane active. */
-__device__ __forceinline__ uint64_t tile_keep(const KParams& p, const PrimBox* boxes) {
+ * tests box l, one ballot.  box_load issues the load (early, so its latency hides behind
+ * ray generation), box_keep does the branch-free compare and the ballot.  All lanes
+ * active. */
+__device__ __forceinline__ uint64_t box_load(const KParams& p, const PrimBox* boxes) {
+    const int l = threadIdx.x & 63;
+    const uint64_t v = *reinterpret_cast<const uint64_t*>(boxes + (l < p.nbox ? l : 0));
+    return l < p.nbox ? v : 0x80007fff80007fffull;  // x0 = i0 = 32767 > x1 = i1: never meets
+}
+__device__ __forceinline__ uint64_t box_keep(const KParams& p, uint64_t raw) {
     const int wave = threadIdx.x >> 6;
     const int tx0 = blockIdx.x * TILE_W + (TILE_W > 8 ? (wave & 1) * 8 : 0);
     const int ty0 = p.row0 + tile_row(p) * TILE_H + (TILE_H > 8 ? (wave >> 1) * 8 : 0);
-    const int l = threadIdx.x & 63;
-    bool hit = false;
-    if (l < p.nbox) {
-        const PrimBox b = boxes[l];
-        hit = b.x0 <= tx0 + 7 && b.x1 >= tx0 && b.i0 <= ty0 + 7 && b.i1 >= ty0;
-    }
+    const int x0 = (int16_t)(raw & 0xffff), x1 = (int16_t)((raw >> 16) & 0xffff);
+    const int i0 = (int16_t)((raw >> 32) & 0xffff), i1 = (int16_t)(raw >> 48);
+    const bool hit = (x0 <= tx0 + 7) & (x1 >= tx0) & (i0 <= ty0 + 7) & (i1 >= ty0);
     return uniform64(__ballot(hit));
 }
-__device__ __forceinline__ uint64_t tile_keep(const KParams& p) { return tile_keep(p, p.box); }
+__device__ __forceinline__ uint64_t tile_keep(const KParams& p, const PrimBox* boxes) {
+    return box_keep(p, box_load(p, boxes));
+}
 
 /* Bounce k <= mir_depth after a chain of wall hits (rt_device.h "mirror bins"): when
  * every live lane's previous k segments hit the same walls in the same order, the wave's
@@ -813,9 +840,17 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
     using CT = typename std::conditional<COLOR64, double, float>::type;
     const d3 cpos = ld3(p.pos);
     const d3 pc = (ld3(p.tl) + ld3(p.dx) * (double)x) + ld3(p.dy) * (double)i;  // main.cpp:132
-    RayD r = make_ray(cpos, cpos - pc);  // main.cpp:133-134 (direction not normalised)
+    const uint64_t braw = CULL ? 0 : box_load(p, p.box);  // branch-free: issued first
+    // main.cpp:133-134 (direction not normalised); the sphere terms only where needed
+    // (PATH64: the fp32 terminal segment needs none of them)
+    constexpr bool LAZY = RT_LAZY_TERMS && !COLOR64 && !CULL && RT_TERMINAL_F32;
+    RayD r = LAZY ? make_ray_lazy(cpos, cpos - pc) : make_ray(cpos, cpos - pc);
+    bool terms = !LAZY;
     constexpr bool sun = SUN;
-    const uint64_t keep = (!CULL && p.nbox > 0) ? tile_keep(p) : ~0ull;  // all lanes active
+    if (RT_BOX_SCHED_BARRIER) __builtin_amdgcn_sched_barrier(0);  // compare after ray gen
+    uint64_t keep = CULL ? ~0ull : box_keep(p, braw);  // all lanes active
+    if (p.nbox == 0) keep = ~0ull;
+    const uint64_t smask = p.nS >= 64 ? ~0ull : (1ull << p.nS) - 1;
 
     CT st_s[MAXD];
     CT st_k[MAXD];
@@ -833,10 +868,18 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
         uint64_t km = ~0ull;
         if (!CULL && k == 0 && p.nbox > 0) km = keep;
         if (!CULL && k >= 1 && k <= p.mir_depth) km = mirror_keep<MAXD>(p, alive, st_m, k);
+        if (LAZY && !terms && (km & smask) != 0) {  // a sphere may be tested
+            ray_terms(r);
+            terms = true;
+        }
         const HitD h = scan_d<MIXED, CULL>(p, r, alive, k == 0, km != ~0ull, km);
+        const bool last = k >= p.depth || k >= MAXD;  // remaining_iterations <= 0 (main.cpp:105)
+        if (LAZY && !terms && __any(alive && !last && h.slot >= 0)) {  // a reflection follows
+            ray_terms(r);
+            terms = true;
+        }
         if (!alive) continue;
         ++segs;
-        const bool last = k >= p.depth || k >= MAXD;  // remaining_iterations <= 0 (main.cpp:105)
         if (!COLOR64 && RT_TERMINAL_F32 && (last || h.slot < 0)) {
             // PATH64, last segment of the path: nothing here feeds another ray
             DIAG(10);
@@ -891,7 +934,8 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
             N = ld3(p.w64[h.slot - p.nS].n);
         }
         const DevMat& m = p.mat[h.slot];
-        const d3 nn = normalize_e(N);
+        // normalize(N): a wall's is a scene constant (host, same IEEE operations)
+        const d3 nn = h.slot < p.nS ? normalize_e(N) : ld3(p.wnn[h.slot - p.nS]);
         CT s, ks;
         if (COLOR64) {
             const ShadeD sh = shade_d<INT_EXP>(m, pos, nn, -nv, sun);
@@ -916,7 +960,12 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
         n = k + 1;
         // start + reflect(d, N) (main.cpp:111-113, vec.cpp:51-57)
         const double cc = 2 * dot(nv, nn);
-        r = make_ray(pos + N * .0001, nv - nn * cc);
+        if (LAZY) {
+            r = make_ray_lazy(pos + N * .0001, nv - nn * cc);
+            terms = false;
+        } else {
+            r = make_ray(pos + N * .0001, nv - nn * cc);
+        }
     }
     for (int q = MAXD - 1; q >= 0; --q) {
         if (q < n) {
@@ -1035,7 +1084,7 @@ __device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, bool
     int st_m[MAXD];
     int n = 0;
     f3 c = F3(0.f, 0.f, 0.f);
-    const uint64_t keep = (!CULL && p.nbox > 0) ? tile_keep(p) : ~0ull;  // all lanes active
+    const uint64_t keep = (!CULL && p.nbox > 0) ? tile_keep(p, p.box) : ~0ull;  // all lanes active
     for (int k = 0;; ++k) {
         if (!__any(alive)) break;
         bounce_priority(k);

@@ -1,3 +1,3 @@
-set -u; export TMPDIR=/tmp; O=gpurun_out/r1b_s7; mkdir -p $O
-timeout -k 10 300 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > $O/pytest.log 2>&1; rc=$?; tail -3 $O/pytest.log; [ $rc -le 1 ] || exit $rc
-timeout -k 10 200 python tools/opt_ab.py --option MIRROR_BINS --values 0,1 --configs c1,c2 --precisions path64,f32,f64
+set -u; export TMPDIR=/tmp; O=gpurun_out/${S:-x}; mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread ${K:+-k "$K"} > $O/pytest.log 2>&1; rc=$?; tail -3 $O/pytest.log; [ $rc -le 1 ] || exit $rc
+timeout -k 10 200 python tools/ab.py --a ray-tracer-from-scratch_amd/lib/ab/prev.so --b ray-tracer-from-scratch_amd/lib/librt_amd.so ${MORE:+--more $MORE} --configs ${CFGS:-c1,c2} --precisions ${PRECS:-path64,f32}
