@@ -186,6 +186,17 @@ int32_t rt_out_bytes_per_pixel(int32_t out_format);
  * blocks for multi-GPU tiling: [*row0, *row0 + *nrows). */
 int rt_band_rows(int32_t height, int32_t nranks, int32_t rank, int32_t* row0, int32_t* nrows);
 
+/* Diagnostics, host only (no device): the per-frame pixel boxes of the tile bins for a
+ * scene and camera, as the linear-scan kernels would receive them (<= 64 primitives, else
+ * *nbox = 0).  out receives 4 int16 per box {x0, x1, i0, i1} (inclusive pixel column and
+ * frame row ranges; x0 > x1 = never hit): the *nbox primary boxes in material-slot order
+ * (spheres in scene order, then walls in scene order, z-normal walls that can never be hit
+ * dropped), then for each mirror level L = 1..*mir_depth the nW^L wall sequences (base-nW
+ * number w1..wL) of *nbox boxes each.  RT_ERR_INVALID_ARG when cap (boxes) is too small
+ * (*nbox and *mir_depth are still set). */
+int rt_frame_boxes(const rt_prim* prims, int32_t n, const rt_camera* cam, int32_t row0,
+                   int32_t nrows, int16_t* out, int32_t cap, int32_t* nbox, int32_t* mir_depth);
+
 /* Largest depth the kernels are compiled for (depth 0..rt_max_depth()). */
 int32_t rt_max_depth(void);
 

@@ -11,6 +11,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <new>
 #include <vector>
 
@@ -24,22 +25,25 @@ struct rt_ctx {
     void* d_scene = nullptr;
     size_t scene_bytes = 0;
     bool have_scene = false;
-    int nS = 0, nW = 0, nP = 0;
-    bool int_exp = true;
+    struct SceneHost {
+        int nS = 0, nW = 0, nP = 0;
+        bool int_exp = true;
+        size_t off_s64 = 0, off_w32 = 0, off_w64 = 0, off_sj = 0, off_wj = 0, off_mat = 0,
+               off_mat32 = 0, off_wnn = 0, total = 0;
+        std::vector<char> bytes;    // the device image of the scene (rt_device.h layout)
+        std::vector<double> h_sph;  // nS x {cx, cy, cz, radius^2, radius}
+        std::vector<double> h_wal;  // nW x {P, n, X, Y, length, width}
+        std::vector<double> h_km;   // metallic of each material slot
+    } sc;
     unsigned long long* d_stats = nullptr;
     int wave_cull_min = 24;  // spheres from which the wave cull pays (tools/sweep.py)
     bool eye_tables = true;  // RT_OPT_EYE_TABLES
     bool tile_bins = true;   // RT_OPT_TILE_BINS
     bool row_order = true;   // RT_OPT_ROW_ORDER
     bool mirror_bins = true; // RT_OPT_MIRROR_BINS
-    std::vector<double> h_km;   // metallic of each material slot
-    size_t off_s64 = 0, off_w32 = 0, off_w64 = 0, off_sj = 0, off_wj = 0, off_mat = 0, off_mat32 = 0,
-           off_wnn = 0;
     void* d_out = nullptr;
     size_t d_out_cap = 0;
     unsigned long long* d_segs = nullptr;
-    std::vector<double> h_sph;  // host copy: nS x {cx, cy, cz, radius^2, radius}
-    std::vector<double> h_wal;  // host copy: nW x {P, n, X, Y, length, width}
     char last_err[256] = {0};
 };
 
@@ -176,8 +180,8 @@ void boxes_for(const rt_ctx* ctx, const Proj& P, double dmax, int32_t width, int
     };
     const double* o = P.o;
     const double oabs = std::fabs(o[0]) + std::fabs(o[1]) + std::fabs(o[2]);
-    for (int s = 0; s < ctx->nS; s++) {
-        const double* S = &ctx->h_sph[5 * s];
+    for (int s = 0; s < ctx->sc.nS; s++) {
+        const double* S = &ctx->sc.h_sph[5 * s];
         const double r = S[4];
         const double v[3] = {S[0] - o[0], S[1] - o[1], S[2] - o[2]};
         const double delta = 1e-6 * (1 + oabs + std::fabs(S[0]) + std::fabs(S[1]) + std::fabs(S[2]) + r);
@@ -201,8 +205,8 @@ void boxes_for(const rt_ctx* ctx, const Proj& P, double dmax, int32_t width, int
         }
         out[s] = b;
     }
-    for (int w = 0; w < ctx->nW; w++) {
-        const double* Wd = &ctx->h_wal[14 * w];
+    for (int w = 0; w < ctx->sc.nW; w++) {
+        const double* Wd = &ctx->sc.h_wal[14 * w];
         const double *Pw = Wd, *n = Wd + 3, *X = Wd + 6, *Y = Wd + 9;
         const double len = Wd[12], wid = Wd[13];
         const double pv[3] = {Pw[0] - o[0], Pw[1] - o[1], Pw[2] - o[2]};
@@ -240,7 +244,7 @@ void boxes_for(const rt_ctx* ctx, const Proj& P, double dmax, int32_t width, int
                 b = to_box(acc);
             }
         }
-        out[ctx->nS + w] = b;
+        out[ctx->sc.nS + w] = b;
     }
 }
 
@@ -248,7 +252,7 @@ void frame_boxes(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t 
                  rt::KParams& p) {
     p.nbox = 0;
     p.mir_depth = 0;
-    const int np = ctx->nS + ctx->nW;
+    const int np = ctx->sc.nS + ctx->sc.nW;
     if (!ctx->tile_bins || p.wave_cull || np == 0 || np > rt::BIN_MAX_PRIMS || cam->width > 32000 ||
         cam->height > 32000 || nrows <= 0 || cam->width <= 0)
         return;
@@ -277,7 +281,7 @@ void frame_boxes(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t 
             const int x0 = std::max<int>(b.x0, 0), x1 = std::min<int>(b.x1, cam->width - 1);
             const int i0 = std::max<int>(b.i0, row0), i1 = std::min<int>(b.i1, row0 + nrows - 1);
             if (x0 > x1 || i0 > i1) continue;
-            const double wgt = (1.0 + 3.0 * ctx->h_km[j]) * (x1 - x0 + 1);
+            const double wgt = (1.0 + 3.0 * ctx->sc.h_km[j]) * (x1 - x0 + 1);
             for (int t = (i0 - row0) / 8; t <= (i1 - row0) / 8; t++) prof[t] += wgt;
         }
         double tot = 0;
@@ -297,7 +301,7 @@ void frame_boxes(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t 
     // but |R d| = |d| keeps dmax.  Only chains some tile can follow are computed (their
     // "reach" — the intersection of the boxes along the chain, widened by a tile — is
     // non-empty); every other sequence keeps all primitives.
-    const int nW = ctx->nW;
+    const int nW = ctx->sc.nW;
     int depth = 0;
     for (long tot = 0, lvl = 1; depth < rt::MIR_MAX_DEPTH && nW > 0; depth++) {
         lvl *= nW;
@@ -338,12 +342,12 @@ void frame_boxes(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t 
                 rt::PrimBox* out = p.mbox + (size_t)(off + q) * np;
                 Node& nd = cur[q];
                 nd.reach = empty(prev[q0].reach) ? prev[q0].reach
-                                                 : meet(prev[q0].reach, widen(prev_boxes[q0][ctx->nS + w]));
+                                                 : meet(prev[q0].reach, widen(prev_boxes[q0][ctx->sc.nS + w]));
                 if (empty(nd.reach)) {
                     for (int j = 0; j < np; j++) out[j] = allb;  // never followed: keep all
                     continue;
                 }
-                const double* Wd = &ctx->h_wal[14 * w];
+                const double* Wd = &ctx->sc.h_wal[14 * w];
                 const double *Pw = Wd, *n = Wd + 3;
                 const Proj& pc = prev[q0].cam;
                 const double op[3] = {pc.o[0] - Pw[0], pc.o[1] - Pw[1], pc.o[2] - Pw[2]};
@@ -370,18 +374,18 @@ rt::KParams make_params(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, i
     rt::KParams p{};
     const char* base = static_cast<const char*>(ctx->d_scene);
     p.s32 = reinterpret_cast<const rt::SphG32*>(base);
-    p.s64 = reinterpret_cast<const rt::SphG64*>(base + ctx->off_s64);
-    p.w32 = reinterpret_cast<const rt::Wall32*>(base + ctx->off_w32);
-    p.w64 = reinterpret_cast<const rt::Wall64*>(base + ctx->off_w64);
-    p.sph_j = reinterpret_cast<const int32_t*>(base + ctx->off_sj);
-    p.wall_j = reinterpret_cast<const int32_t*>(base + ctx->off_wj);
-    p.mat = reinterpret_cast<const rt::DevMat*>(base + ctx->off_mat);
-    p.mat32 = reinterpret_cast<const rt::DevMat32*>(base + ctx->off_mat32);
-    p.wnn = reinterpret_cast<const double(*)[4]>(base + ctx->off_wnn);
-    p.nS = ctx->nS;
-    p.nW = ctx->nW;
-    p.int_exp = ctx->int_exp ? 1 : 0;
-    p.wave_cull = ctx->nS >= ctx->wave_cull_min ? 1 : 0;
+    p.s64 = reinterpret_cast<const rt::SphG64*>(base + ctx->sc.off_s64);
+    p.w32 = reinterpret_cast<const rt::Wall32*>(base + ctx->sc.off_w32);
+    p.w64 = reinterpret_cast<const rt::Wall64*>(base + ctx->sc.off_w64);
+    p.sph_j = reinterpret_cast<const int32_t*>(base + ctx->sc.off_sj);
+    p.wall_j = reinterpret_cast<const int32_t*>(base + ctx->sc.off_wj);
+    p.mat = reinterpret_cast<const rt::DevMat*>(base + ctx->sc.off_mat);
+    p.mat32 = reinterpret_cast<const rt::DevMat32*>(base + ctx->sc.off_mat32);
+    p.wnn = reinterpret_cast<const double(*)[4]>(base + ctx->sc.off_wnn);
+    p.nS = ctx->sc.nS;
+    p.nW = ctx->sc.nW;
+    p.int_exp = ctx->sc.int_exp ? 1 : 0;
+    p.wave_cull = ctx->sc.nS >= ctx->wave_cull_min ? 1 : 0;
     p.W = cam->width;
     p.row0 = row0;
     p.nrows = nrows;
@@ -399,18 +403,18 @@ rt::KParams make_params(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, i
     p.stats = ctx->d_stats;
     // eye tables (rt_device.h) for the linear-scan kernels: the same fp64 operations, in
     // the same order, as sphere_exact / wall_exact on a ray starting at cam->position
-    p.eye = (ctx->eye_tables && !p.wave_cull && ctx->nS <= rt::EYE_MAX_S && ctx->nW <= rt::EYE_MAX_W) ? 1 : 0;
+    p.eye = (ctx->eye_tables && !p.wave_cull && ctx->sc.nS <= rt::EYE_MAX_S && ctx->sc.nW <= rt::EYE_MAX_W) ? 1 : 0;
     if (p.eye) {
         const double* o = cam->position;
-        for (int s = 0; s < ctx->nS; s++) {
-            const double* S = &ctx->h_sph[5 * s];
+        for (int s = 0; s < ctx->sc.nS; s++) {
+            const double* S = &ctx->sc.h_sph[5 * s];
             const double ox = o[0] - S[0], oy = o[1] - S[1], oz = o[2] - S[2];  // scene.cpp:45
             const double c = (ox * ox + oy * oy + oz * oz) - S[3];              // scene.cpp:51
             const double e[4] = {ox, oy, oz, c};
             for (int k = 0; k < 4; k++) p.eye_s[s][k] = e[k];
         }
-        for (int w = 0; w < ctx->nW; w++) {
-            const double* P = &ctx->h_wal[14 * w];
+        for (int w = 0; w < ctx->sc.nW; w++) {
+            const double* P = &ctx->sc.h_wal[14 * w];
             const double* n = P + 3;
             p.eye_w[w] = (P[0] - o[0]) * n[0] + (P[1] - o[1]) * n[1] + (P[2] - o[2]) * n[2];  // scene.cpp:10
         }
@@ -418,6 +422,151 @@ rt::KParams make_params(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, i
     frame_boxes(ctx, cam, row0, nrows, p);
     return p;
 }
+
+/* rt_set_scene's host half: the device image of the scene (rt_device.h layout) and the
+ * host copies the per-frame boxes and eye tables use.  No device call. */
+int pack_scene(const rt_prim* prims, int32_t n, rt_ctx::SceneHost& sc) {
+    if (n < 0 || (n > 0 && !prims)) return RT_ERR_INVALID_ARG;
+    struct Sph {
+        double c[3], r;
+        int32_t j;
+    };
+    struct Wal {
+        double P[3], n[3], X[3], Y[3], len, wid;
+        int32_t j;
+    };
+    std::vector<Sph> sph;
+    std::vector<Wal> wal;
+    for (int32_t j = 0; j < n; j++) {
+        const rt_prim& q = prims[j];
+        if (q.reserved != 0) return RT_ERR_INVALID_ARG;
+        if (q.kind == RT_PRIM_SPHERE) {
+            sph.push_back(Sph{{q.position[0], q.position[1], q.position[2]}, q.radius, j});
+        } else if (q.kind == RT_PRIM_WALL) {
+            const hv3 nrm{q.normal[0], q.normal[1], q.normal[2]};
+            const hv3 X = hnormalize(hcross(nrm, hv3{0, 0, 1}));  // scene.cpp:18
+            const hv3 Y = hnormalize(hcross(X, nrm));             // scene.cpp:19
+            // A NaN basis (normal parallel to z) or NaN normal makes every projection NaN:
+            // the reference can never report a hit for this wall, so it is not uploaded.
+            if (hnan(X) || hnan(Y) || hnan(nrm)) continue;
+            wal.push_back(Wal{{q.position[0], q.position[1], q.position[2]},
+                              {nrm.x, nrm.y, nrm.z}, {X.x, X.y, X.z}, {Y.x, Y.y, Y.z},
+                              q.length, q.width, j});
+        } else {
+            return RT_ERR_INVALID_ARG;
+        }
+    }
+    const size_t nS = sph.size(), nW = wal.size(), ng = (nS + 3) / 4;
+    const size_t off_s64 = align_up(ng * sizeof(rt::SphG32), 256);
+    const size_t off_w32 = align_up(off_s64 + ng * sizeof(rt::SphG64), 256);
+    const size_t off_w64 = align_up(off_w32 + nW * sizeof(rt::Wall32), 256);
+    const size_t off_sj = align_up(off_w64 + nW * sizeof(rt::Wall64), 256);
+    const size_t off_wj = align_up(off_sj + nS * sizeof(int32_t), 256);
+    const size_t off_mat = align_up(off_wj + nW * sizeof(int32_t), 256);
+    const size_t off_mat32 = align_up(off_mat + (nS + nW) * sizeof(rt::DevMat), 256);
+    const size_t off_wnn = align_up(off_mat32 + (nS + nW) * sizeof(rt::DevMat32), 256);
+    const size_t total = align_up(off_wnn + nW * 4 * sizeof(double), 256) + 256;
+    sc.bytes.assign(total, 0);
+    sc.total = total;
+    std::vector<char>& host = sc.bytes;
+    auto* s32 = reinterpret_cast<rt::SphG32*>(host.data());
+    auto* s64 = reinterpret_cast<rt::SphG64*>(host.data() + off_s64);
+    auto* w32 = reinterpret_cast<rt::Wall32*>(host.data() + off_w32);
+    auto* w64 = reinterpret_cast<rt::Wall64*>(host.data() + off_w64);
+    auto* sj = reinterpret_cast<int32_t*>(host.data() + off_sj);
+    auto* wj = reinterpret_cast<int32_t*>(host.data() + off_wj);
+    auto* mat = reinterpret_cast<rt::DevMat*>(host.data() + off_mat);
+    auto* mat32 = reinterpret_cast<rt::DevMat32*>(host.data() + off_mat32);
+    auto* wnn = reinterpret_cast<double(*)[4]>(host.data() + off_wnn);
+    auto put_mat = [&](size_t slot, const rt_material& m) {
+        rt::DevMat& d = mat[slot];
+        for (int k = 0; k < 3; k++) d.color[k] = m.color[k];
+        d.ka = m.ambient;
+        d.km = m.metallic;
+        d.kd = m.diffuse;
+        d.ks = m.specular;
+        d.ex = m.specular_exponent;
+        rt::DevMat32& f = mat32[slot];
+        for (int k = 0; k < 3; k++) f.color[k] = (float)m.color[k];
+        f.ka = (float)m.ambient;
+        f.km = (float)m.metallic;
+        f.kd = (float)m.diffuse;
+        f.ks = (float)m.specular;
+        f.ex = (float)m.specular_exponent;
+    };
+    for (size_t s = 0; s < nS; s++) {
+        rt::SphG32& g = s32[s / 4];
+        double* d = s64[s / 4].v[s % 4];
+        for (int k = 0; k < 3; k++) {
+            g.c[k][s % 4] = (float)sph[s].c[k];
+            d[k] = sph[s].c[k];
+        }
+        g.c[3][s % 4] = (float)sph[s].r;
+        d[3] = sph[s].r * sph[s].r;  // scene.cpp:51
+        sj[s] = sph[s].j;
+        put_mat(s, prims[sph[s].j].mat);
+    }
+    for (size_t w = 0; w < nW; w++) {
+        const Wal& a = wal[w];
+        for (int k = 0; k < 3; k++) {
+            w64[w].P[k] = a.P[k];
+            w64[w].n[k] = a.n[k];
+            w64[w].X[k] = a.X[k];
+            w64[w].Y[k] = a.Y[k];
+            w32[w].P[k] = (float)a.P[k];
+            w32[w].n[k] = (float)a.n[k];
+            w32[w].X[k] = (float)a.X[k];
+            w32[w].Y[k] = (float)a.Y[k];
+        }
+        w64[w].len = a.len;
+        w64[w].wid = a.wid;
+        w32[w].len = (float)a.len;
+        w32[w].wid = (float)a.wid;
+        wj[w] = a.j;
+        put_mat(nS + w, prims[a.j].mat);
+        const hv3 nn = hnormalize(hv3{a.n[0], a.n[1], a.n[2]});  // N.normalize(), vec.cpp:21
+        wnn[w][0] = nn.x;
+        wnn[w][1] = nn.y;
+        wnn[w][2] = nn.z;
+    }
+
+    sc.nS = (int)nS;
+    sc.nW = (int)nW;
+    sc.nP = n;
+    sc.int_exp = true;
+    for (size_t k = 0; k < nS + nW; k++) {
+        const double e = mat[k].ex;
+        if (!(e >= 0.0 && e <= 1024.0 && e == std::floor(e))) sc.int_exp = false;
+    }
+    sc.h_km.assign(nS + nW, 0.0);
+    for (size_t k = 0; k < nS + nW; k++) sc.h_km[k] = mat[k].km;
+    sc.h_sph.assign(5 * nS, 0.0);
+    for (size_t s = 0; s < nS; s++) {
+        for (int k = 0; k < 4; k++) sc.h_sph[5 * s + k] = s64[s / 4].v[s % 4][k];
+        sc.h_sph[5 * s + 4] = sph[s].r;
+    }
+    sc.h_wal.assign(14 * nW, 0.0);
+    for (size_t w = 0; w < nW; w++) {
+        for (int k = 0; k < 3; k++) {
+            sc.h_wal[14 * w + k] = w64[w].P[k];
+            sc.h_wal[14 * w + 3 + k] = w64[w].n[k];
+            sc.h_wal[14 * w + 6 + k] = w64[w].X[k];
+            sc.h_wal[14 * w + 9 + k] = w64[w].Y[k];
+        }
+        sc.h_wal[14 * w + 12] = w64[w].len;
+        sc.h_wal[14 * w + 13] = w64[w].wid;
+    }
+    sc.off_s64 = off_s64;
+    sc.off_w32 = off_w32;
+    sc.off_w64 = off_w64;
+    sc.off_sj = off_sj;
+    sc.off_wj = off_wj;
+    sc.off_mat = off_mat;
+    sc.off_mat32 = off_mat32;
+    sc.off_wnn = off_wnn;
+    return RT_OK;
+}
+
 
 }  // namespace
 
@@ -539,152 +688,47 @@ int rt_ctx_destroy(rt_ctx* ctx) {
 
 int rt_set_scene(rt_ctx* ctx, const rt_prim* prims, int32_t n) {
     if (!ctx || n < 0 || (n > 0 && !prims)) return RT_ERR_INVALID_ARG;
-    struct Sph {
-        double c[3], r;
-        int32_t j;
-    };
-    struct Wal {
-        double P[3], n[3], X[3], Y[3], len, wid;
-        int32_t j;
-    };
-    std::vector<Sph> sph;
-    std::vector<Wal> wal;
-    for (int32_t j = 0; j < n; j++) {
-        const rt_prim& q = prims[j];
-        if (q.reserved != 0) return RT_ERR_INVALID_ARG;
-        if (q.kind == RT_PRIM_SPHERE) {
-            sph.push_back(Sph{{q.position[0], q.position[1], q.position[2]}, q.radius, j});
-        } else if (q.kind == RT_PRIM_WALL) {
-            const hv3 nrm{q.normal[0], q.normal[1], q.normal[2]};
-            const hv3 X = hnormalize(hcross(nrm, hv3{0, 0, 1}));  // scene.cpp:18
-            const hv3 Y = hnormalize(hcross(X, nrm));             // scene.cpp:19
-            // A NaN basis (normal parallel to z) or NaN normal makes every projection NaN:
-            // the reference can never report a hit for this wall, so it is not uploaded.
-            if (hnan(X) || hnan(Y) || hnan(nrm)) continue;
-            wal.push_back(Wal{{q.position[0], q.position[1], q.position[2]},
-                              {nrm.x, nrm.y, nrm.z}, {X.x, X.y, X.z}, {Y.x, Y.y, Y.z},
-                              q.length, q.width, j});
-        } else {
-            return RT_ERR_INVALID_ARG;
-        }
-    }
-    const size_t nS = sph.size(), nW = wal.size(), ng = (nS + 3) / 4;
-    const size_t off_s64 = align_up(ng * sizeof(rt::SphG32), 256);
-    const size_t off_w32 = align_up(off_s64 + ng * sizeof(rt::SphG64), 256);
-    const size_t off_w64 = align_up(off_w32 + nW * sizeof(rt::Wall32), 256);
-    const size_t off_sj = align_up(off_w64 + nW * sizeof(rt::Wall64), 256);
-    const size_t off_wj = align_up(off_sj + nS * sizeof(int32_t), 256);
-    const size_t off_mat = align_up(off_wj + nW * sizeof(int32_t), 256);
-    const size_t off_mat32 = align_up(off_mat + (nS + nW) * sizeof(rt::DevMat), 256);
-    const size_t off_wnn = align_up(off_mat32 + (nS + nW) * sizeof(rt::DevMat32), 256);
-    const size_t total = align_up(off_wnn + nW * 4 * sizeof(double), 256) + 256;
-    std::vector<char> host(total, 0);
-    auto* s32 = reinterpret_cast<rt::SphG32*>(host.data());
-    auto* s64 = reinterpret_cast<rt::SphG64*>(host.data() + off_s64);
-    auto* w32 = reinterpret_cast<rt::Wall32*>(host.data() + off_w32);
-    auto* w64 = reinterpret_cast<rt::Wall64*>(host.data() + off_w64);
-    auto* sj = reinterpret_cast<int32_t*>(host.data() + off_sj);
-    auto* wj = reinterpret_cast<int32_t*>(host.data() + off_wj);
-    auto* mat = reinterpret_cast<rt::DevMat*>(host.data() + off_mat);
-    auto* mat32 = reinterpret_cast<rt::DevMat32*>(host.data() + off_mat32);
-    auto* wnn = reinterpret_cast<double(*)[4]>(host.data() + off_wnn);
-    auto put_mat = [&](size_t slot, const rt_material& m) {
-        rt::DevMat& d = mat[slot];
-        for (int k = 0; k < 3; k++) d.color[k] = m.color[k];
-        d.ka = m.ambient;
-        d.km = m.metallic;
-        d.kd = m.diffuse;
-        d.ks = m.specular;
-        d.ex = m.specular_exponent;
-        rt::DevMat32& f = mat32[slot];
-        for (int k = 0; k < 3; k++) f.color[k] = (float)m.color[k];
-        f.ka = (float)m.ambient;
-        f.km = (float)m.metallic;
-        f.kd = (float)m.diffuse;
-        f.ks = (float)m.specular;
-        f.ex = (float)m.specular_exponent;
-    };
-    for (size_t s = 0; s < nS; s++) {
-        rt::SphG32& g = s32[s / 4];
-        double* d = s64[s / 4].v[s % 4];
-        for (int k = 0; k < 3; k++) {
-            g.c[k][s % 4] = (float)sph[s].c[k];
-            d[k] = sph[s].c[k];
-        }
-        g.c[3][s % 4] = (float)sph[s].r;
-        d[3] = sph[s].r * sph[s].r;  // scene.cpp:51
-        sj[s] = sph[s].j;
-        put_mat(s, prims[sph[s].j].mat);
-    }
-    for (size_t w = 0; w < nW; w++) {
-        const Wal& a = wal[w];
-        for (int k = 0; k < 3; k++) {
-            w64[w].P[k] = a.P[k];
-            w64[w].n[k] = a.n[k];
-            w64[w].X[k] = a.X[k];
-            w64[w].Y[k] = a.Y[k];
-            w32[w].P[k] = (float)a.P[k];
-            w32[w].n[k] = (float)a.n[k];
-            w32[w].X[k] = (float)a.X[k];
-            w32[w].Y[k] = (float)a.Y[k];
-        }
-        w64[w].len = a.len;
-        w64[w].wid = a.wid;
-        w32[w].len = (float)a.len;
-        w32[w].wid = (float)a.wid;
-        wj[w] = a.j;
-        put_mat(nS + w, prims[a.j].mat);
-        const hv3 nn = hnormalize(hv3{a.n[0], a.n[1], a.n[2]});  // N.normalize(), vec.cpp:21
-        wnn[w][0] = nn.x;
-        wnn[w][1] = nn.y;
-        wnn[w][2] = nn.z;
-    }
-
+    rt_ctx::SceneHost sc;
+    const int st = pack_scene(prims, n, sc);
+    if (st != RT_OK) return st;
     RT_HIP(ctx, hipSetDevice(ctx->device));
     RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    if (total > ctx->scene_bytes) {
+    if (sc.total > ctx->scene_bytes) {
         if (ctx->d_scene) RT_HIP(ctx, hipFree(ctx->d_scene));
         ctx->d_scene = nullptr;
         ctx->scene_bytes = 0;
-        RT_HIP(ctx, hipMalloc(&ctx->d_scene, total));
-        ctx->scene_bytes = total;
+        RT_HIP(ctx, hipMalloc(&ctx->d_scene, sc.total));
+        ctx->scene_bytes = sc.total;
     }
-    RT_HIP(ctx, hipMemcpy(ctx->d_scene, host.data(), total, hipMemcpyHostToDevice));
-    ctx->nS = (int)nS;
-    ctx->nW = (int)nW;
-    ctx->nP = n;
-    ctx->int_exp = true;
-    for (size_t k = 0; k < nS + nW; k++) {
-        const double e = mat[k].ex;
-        if (!(e >= 0.0 && e <= 1024.0 && e == std::floor(e))) ctx->int_exp = false;
-    }
-    ctx->h_km.assign(nS + nW, 0.0);
-    for (size_t k = 0; k < nS + nW; k++) ctx->h_km[k] = mat[k].km;
-    ctx->h_sph.assign(5 * nS, 0.0);
-    for (size_t s = 0; s < nS; s++) {
-        for (int k = 0; k < 4; k++) ctx->h_sph[5 * s + k] = s64[s / 4].v[s % 4][k];
-        ctx->h_sph[5 * s + 4] = sph[s].r;
-    }
-    ctx->h_wal.assign(14 * nW, 0.0);
-    for (size_t w = 0; w < nW; w++) {
-        for (int k = 0; k < 3; k++) {
-            ctx->h_wal[14 * w + k] = w64[w].P[k];
-            ctx->h_wal[14 * w + 3 + k] = w64[w].n[k];
-            ctx->h_wal[14 * w + 6 + k] = w64[w].X[k];
-            ctx->h_wal[14 * w + 9 + k] = w64[w].Y[k];
-        }
-        ctx->h_wal[14 * w + 12] = w64[w].len;
-        ctx->h_wal[14 * w + 13] = w64[w].wid;
-    }
-    ctx->off_s64 = off_s64;
-    ctx->off_w32 = off_w32;
-    ctx->off_w64 = off_w64;
-    ctx->off_sj = off_sj;
-    ctx->off_wj = off_wj;
-    ctx->off_mat = off_mat;
-    ctx->off_mat32 = off_mat32;
-    ctx->off_wnn = off_wnn;
+    RT_HIP(ctx, hipMemcpy(ctx->d_scene, sc.bytes.data(), sc.total, hipMemcpyHostToDevice));
+    ctx->sc = std::move(sc);
     ctx->have_scene = true;
+    return RT_OK;
+}
+
+int rt_frame_boxes(const rt_prim* prims, int32_t n, const rt_camera* cam, int32_t row0,
+                   int32_t nrows, int16_t* out, int32_t cap, int32_t* nbox, int32_t* mir_depth) {
+    if (!cam || !nbox || !mir_depth || cap < 0 || (cap > 0 && !out)) return RT_ERR_INVALID_ARG;
+    if (row0 < 0 || nrows < 0 || row0 + nrows > cam->height) return RT_ERR_OUT_OF_RANGE;
+    std::unique_ptr<rt_ctx> ctx(new (std::nothrow) rt_ctx());  // host-only: no device resources
+    if (!ctx) return RT_ERR_OUT_OF_MEMORY;
+    const int st = pack_scene(prims, n, ctx->sc);
+    if (st != RT_OK) return st;
+    ctx->wave_cull_min = 0x7fffffff;  // as the linear-scan kernels see the scene
+    std::unique_ptr<rt::KParams> p(new (std::nothrow) rt::KParams);
+    if (!p) return RT_ERR_OUT_OF_MEMORY;
+    *p = make_params(ctx.get(), cam, row0, nrows, 0, 0, RT_OUT_RGB_F32, nullptr, nullptr);
+    long total = p->nbox;
+    for (long L = 1, lvl = 1; L <= p->mir_depth; L++) {
+        lvl *= ctx->sc.nW;
+        total += lvl * p->nbox;
+    }
+    *nbox = p->nbox;
+    *mir_depth = p->mir_depth;
+    if (total > cap) return RT_ERR_INVALID_ARG;
+    for (int j = 0; j < p->nbox; j++) std::memcpy(out + 4 * j, &p->box[j], sizeof(rt::PrimBox));
+    for (long j = p->nbox; j < total; j++)
+        std::memcpy(out + 4 * j, &p->mbox[j - p->nbox], sizeof(rt::PrimBox));
     return RT_OK;
 }
 

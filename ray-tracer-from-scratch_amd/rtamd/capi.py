@@ -112,6 +112,9 @@ SIGNATURES = [
     ("rt_band_rows", C.c_int,
      [C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     ("rt_max_depth", C.c_int32, []),
+    ("rt_frame_boxes", C.c_int,
+     [C.POINTER(rt_prim), C.c_int32, C.POINTER(rt_camera), C.c_int32, C.c_int32,
+      C.POINTER(C.c_int16), C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     ("rt_selftest", C.c_int, [C.c_void_p, C.c_int32, C.c_uint64, C.c_uint64,
                               C.POINTER(C.c_uint64)]),
 ]
@@ -171,6 +174,25 @@ def camera_init(position, lookat, vup, vfov: float, aspect_ratio: float,
     check(lib.rt_camera_init(_d3(position), _d3(lookat), _d3(vup), float(vfov),
                              float(aspect_ratio), float(image_width), C.byref(cam)))
     return cam
+
+
+def frame_boxes(prims, cam: rt_camera, row0: int = 0, nrows: int | None = None):
+    """rt_frame_boxes (host only) -> (primary [nbox, 4], mirror [.., 4], mir_depth): int16
+    {x0, x1, i0, i1} boxes; the mirror array holds the levels back to back (the caller
+    knows nW: level L has nW**L sequences of nbox boxes).  See include/rt_capi.h."""
+    import numpy as np
+    lib = load()
+    if nrows is None:
+        nrows = cam.height - row0
+    arr = (rt_prim * max(1, len(prims)))(*prims)
+    nb, md = C.c_int32(), C.c_int32()
+    cap = 64 * (1 + 8 + 64 + 512)
+    out = np.zeros((cap, 4), np.int16)
+    check(lib.rt_frame_boxes(arr, len(prims), C.byref(cam), row0, nrows,
+                             out.ctypes.data_as(C.POINTER(C.c_int16)), cap, C.byref(nb),
+                             C.byref(md)))
+    n = nb.value
+    return out[:n], out[n:], md.value
 
 
 def band_rows(height: int, nranks: int, rank: int) -> tuple[int, int]:
