@@ -11,6 +11,7 @@
  * use (device/precision from rt_scene_set_options); like the reference, rt_scene is
  * meant to be called from one thread.
  */
+#include <cstring>
 #include <memory>
 #include <mutex>
 #include <stdexcept>
@@ -27,6 +28,7 @@ struct Global {
     rt_ctx* ctx = nullptr;
     int ctx_device = -1;
     std::vector<double> staging;
+    std::vector<rt_prim> uploaded;  // the scene on the device (re-uploaded only on change)
     ~Global() {
         if (ctx) rt_ctx_destroy(ctx);
     }
@@ -66,10 +68,18 @@ void rt_scene(std::vector<vec3> u, const std::vector<std::unique_ptr<SceneGeomet
         g.ctx = nullptr;
         check(rt_ctx_create(g.opts.device, &g.ctx), nullptr, "rt_ctx_create");
         g.ctx_device = g.opts.device;
+        g.uploaded.clear();
     }
+    // the interactive loop renders the same scene frame after frame (main.cpp:329): keep it
+    // resident on the device and upload only when the packed records change
     std::vector<rt_prim> prims(scene.size());
     for (size_t j = 0; j < scene.size(); j++) scene[j]->pack(&prims[j]);
-    check(rt_set_scene(g.ctx, prims.data(), (int32_t)prims.size()), g.ctx, "rt_set_scene");
+    if (g.uploaded.empty() || prims.size() != g.uploaded.size() ||
+        std::memcmp(prims.data(), g.uploaded.data(), prims.size() * sizeof(rt_prim)) != 0) {
+        g.uploaded.clear();
+        check(rt_set_scene(g.ctx, prims.data(), (int32_t)prims.size()), g.ctx, "rt_set_scene");
+        g.uploaded = prims;
+    }
 
     rt_camera c{};
     const vec3* v[4] = {&cam.position, &cam.image_top_left, &u.at(0), &u.at(1)};

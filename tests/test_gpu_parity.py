@@ -471,6 +471,49 @@ def test_row_order_is_output_invariant(rend):
         rend.set_option(capi.RT_OPT_ROW_ORDER, 1)
 
 
+# ---------------------------------------------------------------- headless frame loop
+def _read_ppm(path):
+    with open(path, "rb") as fh:
+        data = fh.read()
+    magic, w, h, mx, rest = data.split(maxsplit=4)
+    assert magic == b"P6" and mx == b"255"
+    return np.frombuffer(rest, np.uint8).reshape(int(h), int(w), 3)
+
+
+def test_frame_loop_binary(tmp_path, oracle):
+    """bin/rt_frames (host/rt_frames.cpp): main.cpp's loop without SDL — scripted camera
+    moves (init() not re-called: stale image_top_left), rt_scene per frame, the
+    SDL_MapRGB packing, and main.cpp's performance log.  The last frame equals the
+    oracle's fp64 frame quantised the same way, with rt_scene (mixed = fp64 path) and with
+    the kernel's RGBA8 epilogue (--gpu-surface)."""
+    import re
+    import subprocess
+    from conftest import PKG
+    exe = os.path.join(PKG, "bin", "rt_frames")
+    outs = {}
+    for mode in ("host", "gpu"):
+        ppm = str(tmp_path / f"{mode}.ppm")
+        cmd = [exe, "--frames", "3", "--width", "64", "--keys", "wd", "--precision", "mixed",
+               "--ppm", ppm] + (["--gpu-surface"] if mode == "gpu" else [])
+        res = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
+        assert res.returncode == 0, res.stderr
+        lines = res.stdout.strip().splitlines()
+        assert re.fullmatch(r"Number of frames: 3 : \d+ ms average frame time", lines[0]), lines
+        for ln, unit, what in zip(lines[1:], ["microseconds"] * 3 + ["milliseconds"] * 2,
+                                  ["raytracing", "outpainting", "shading", "surface average update",
+                                   "SDL rendering"]):
+            assert re.fullmatch(rf"   \d+ {unit} for (average )?{what}", ln), ln
+        outs[mode] = _read_ppm(ppm)
+    assert np.array_equal(outs["host"], outs["gpu"])
+    # expected: frames 'w', 'd', 'w' move the camera (scene.cpp:108-165), init() once
+    cam = capi.camera_init((0, 0, 0), (-1, 0, 0), (0, 0, -1), 90.0, 1.0, 64.0)
+    cam.position[0] = 0.1 + 0.1
+    cam.position[1] = 0.1
+    ref64, _, _ = oracle.render(scenes.to_prims(scenes.default_scene()), cam, 10)
+    q = (np.clip(ref64 * 255.0, 0.0, 255.0)).astype(np.uint8)
+    assert np.array_equal(outs["host"], q)
+
+
 # ---------------------------------------------------------------- multi-GPU path (1 rank)
 def test_render_tiled_rccl_single_rank(rend):
     """rtamd.tiling.render_tiled over the nccl (RCCL) backend with one rank: the gathered
