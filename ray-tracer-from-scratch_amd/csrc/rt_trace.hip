@@ -89,6 +89,9 @@ __device__ unsigned long long g_diag[16];
 #ifndef RT_WPE_PATH64_LIN_BONUS
 #define RT_WPE_PATH64_LIN_BONUS 0
 #endif
+#ifndef RT_WPE_MIXED_CULL_DROP  // MIXED cull kernels at depth > 4: one wave less
+#define RT_WPE_MIXED_CULL_DROP 1
+#endif
 #ifndef RT_WPE_F64_LIN_BONUS
 #define RT_WPE_F64_LIN_BONUS 0
 #endif
@@ -934,8 +937,10 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
             N = ld3(p.w64[h.slot - p.nS].n);
         }
         const DevMat& m = p.mat[h.slot];
-        // normalize(N): a wall's is a scene constant (host, same IEEE operations)
-        const d3 nn = h.slot < p.nS ? normalize_e(N) : ld3(p.wnn[h.slot - p.nS]);
+        // normalize(N): a wall's is a scene constant (host, same IEEE operations); the MIXED
+        // cull kernels keep recomputing it (the select costs them 4 VGPRs and a wave/SIMD)
+        const d3 nn = (h.slot < p.nS || (MIXED && CULL)) ? normalize_e(N)
+                                                           : ld3(p.wnn[h.slot - p.nS]);
         CT s, ks;
         if (COLOR64) {
             const ShadeD sh = shade_d<INT_EXP>(m, pos, nn, -nv, sun);
@@ -1263,7 +1268,7 @@ constexpr int waves_per_eu() {
             ((!CULL && !SUN && tier == 0) ? RT_WPE_PATH64_LIN_BONUS : 0);
     else
         w = (INT_EXP ? (SUN ? 3 : 4) : (SUN ? 2 : 3)) - (tier > 0 ? 1 : 0) -
-            ((PREC == PREC_MIXED && CULL && MAXD >= 8) ? 1 : 0);  // A/B: F64 faster at 4
+            ((PREC == PREC_MIXED && CULL && MAXD >= 8) ? RT_WPE_MIXED_CULL_DROP : 0);
     return w < 2 ? 2 : w;
 }
 
