@@ -105,7 +105,10 @@ constexpr int BIN_MAX_PRIMS = 64;
 // follow.  Sequence (w1..wL) of level L: boxes at mbox[(off_L + q) * nbox ..], q the
 // base-nW number w1..wL, off_L = nW + nW^2 + .. + nW^(L-1).
 constexpr int MIR_MAX_DEPTH = 3;
-constexpr int MIR_MAX_BOXES = 1024;
+#ifndef RT_MIR_MAX_BOXES
+#define RT_MIR_MAX_BOXES 1024
+#endif
+constexpr int MIR_MAX_BOXES = RT_MIR_MAX_BOXES;
 struct PrimBox {
     int16_t x0, x1, i0, i1;  // inclusive pixel box (frame rows); x0 > x1 = never hit
 };

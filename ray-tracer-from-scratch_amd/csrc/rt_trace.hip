@@ -62,6 +62,9 @@
 #ifndef RT_BOX_SCHED_BARRIER
 #define RT_BOX_SCHED_BARRIER 1
 #endif
+#ifndef RT_UNWIND_KEND
+#define RT_UNWIND_KEND 1
+#endif
 #ifndef RT_WAVE_TIMES      // diagnostic build: per-wave start/end stamps into KParams::stats
 #define RT_WAVE_TIMES 0    // (tools/wave_times.py); never on in the product
 #endif
@@ -863,8 +866,12 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
     f3 c32 = F3(0.f, 0.f, 0.f);
     // Converged bounce loop: lanes whose path ended stay (alive == false) so the wave can
     // reduce over its live rays; k is wave-uniform.
+    int kend = 0;  // wave-uniform: bounce iterations run (every lane's n <= kend)
     for (int k = 0;; ++k) {
-        if (!__any(alive)) break;
+        if (!__any(alive)) {
+            kend = k;
+            break;
+        }
         bounce_priority(k);
         // tile bins: the primary segment, and the first bounce when the whole wave
         // reflected off one wall (both wave-uniform)
@@ -973,7 +980,7 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
         }
     }
     for (int q = MAXD - 1; q >= 0; --q) {
-        if (q < n) {
+        if ((!RT_UNWIND_KEND || q < kend) && q < n) {  // uniform test: levels no lane reached
             const DevMat& m = p.mat[st_m[q]];
             if (COLOR64) {
                 const d3 L = local_color_d(m, st_s[q], st_k[q], sun);
@@ -1090,8 +1097,12 @@ __device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, bool
     int n = 0;
     f3 c = F3(0.f, 0.f, 0.f);
     const uint64_t keep = (!CULL && p.nbox > 0) ? tile_keep(p, p.box) : ~0ull;  // all lanes active
+    int kend = 0;  // wave-uniform: bounce iterations run (every lane's n <= kend)
     for (int k = 0;; ++k) {
-        if (!__any(alive)) break;
+        if (!__any(alive)) {
+            kend = k;
+            break;
+        }
         bounce_priority(k);
         const float a = fdot(d, d);
         const float ra = frcp(a);
@@ -1201,7 +1212,7 @@ __device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, bool
         d = fmad3(nn, -cc, nv);
     }
     for (int q = MAXD - 1; q >= 0; --q) {
-        if (q < n) {
+        if ((!RT_UNWIND_KEND || q < kend) && q < n) {  // uniform test: levels no lane reached
             const DevMat32& m = p.mat32[st_m[q]];
             const f3 L = local_color_f(m, st_s[q], st_k[q], sun);
             const float km = m.km;
