@@ -62,6 +62,9 @@
 #ifndef RT_BOX_SCHED_BARRIER
 #define RT_BOX_SCHED_BARRIER 1
 #endif
+#ifndef RT_WALL_PAIRS      // exact wall tests two at a time in one basic block (ILP)
+#define RT_WALL_PAIRS 0    // A/B: +10% at c2 (lost t-skip, +16 VGPRs), off
+#endif
 #ifndef RT_UNWIND_KEND
 #define RT_UNWIND_KEND 1
 #endif
@@ -336,6 +339,46 @@ __device__ __forceinline__ void wall_exact(const Wall64& Wl, int w, const KParam
     }
 }
 
+/* The same test as wall_exact without its early exits, for two walls evaluated in one
+ * basic block (independent dependency chains the scheduler can interleave: a wave's
+ * scan is latency-bound on its critical path).  For lanes that pass the sign test t is
+ * bit-identical to wall_exact's; ok = the reference reports a hit at parametric t. */
+template <bool EYE>
+__device__ __forceinline__ void wall_eval(const Wall64& Wl, int w, const KParams& p,
+                                          const RayD& r, double& t, bool& ok) {
+    const d3 n = ld3(Wl.n);
+    const d3 P = ld3(Wl.P);
+    const double den = dot(n, r.d);
+    const double num = EYE ? p.eye_w[w] : dot(P - r.o, n);
+    const bool sgn = (num > 0 && den > 0) || (num < 0 && den < 0);
+    const double dd = sgn ? den : 1.0;  // masked lanes: any finite divisor
+    t = div_r(num, dd, rcp_refined(dd));
+    const d3 q = (r.o + r.d * t) - P;
+    const double px = dot(q, ld3(Wl.X));
+    const double py = dot(q, ld3(Wl.Y));
+    ok = sgn && t > 0 && px >= 0 && px <= Wl.len && py >= 0 && py <= Wl.wid;
+}
+__device__ __forceinline__ void wall_take(const KParams& p, int w, double t, bool ok, HitD& h) {
+    if (!ok) return;
+    bool take = t < h.dist;
+    if (!take && t == h.dist && h.slot >= 0)  // tie: the lower scene index wins (rare)
+        take = p.wall_j[w] < scene_index(p, h.slot);
+    if (take) {
+        h.dist = t;
+        h.slot = p.nS + w;
+    }
+}
+template <bool EYE>
+__device__ __forceinline__ void wall_pair(const KParams& p, int w0, int w1, const RayD& r,
+                                          HitD& h) {
+    double t0, t1;
+    bool ok0, ok1;
+    wall_eval<EYE>(p.w64[w0], w0, p, r, t0, ok0);
+    wall_eval<EYE>(p.w64[w1], w1, p, r, t1, ok1);
+    wall_take(p, w0, t0, ok0, h);  // scene order
+    wall_take(p, w1, t1, ok1, h);
+}
+
 /* MIXED: fp32 conservative cull in front of the exact sphere test.  A sphere is skipped
  * only when the fp32 evaluation proves, with a margin covering its rounding error, that
  * the exact test rejects it (det < 0, or b > 0).  Margins:
@@ -538,6 +581,11 @@ __device__ __forceinline__ void sphere_by_index(const KParams& p, int s, const R
 template <bool MIXED, bool EYE = false>
 __device__ __forceinline__ void walls_d(const KParams& p, const RayD& r, const RayF& rf, HitD& h) {
     for (int w = 0; w < p.nW; ++w) {
+        if (!MIXED && RT_WALL_PAIRS && w + 1 < p.nW) {
+            wall_pair<EYE>(p, w, w + 1, r, h);
+            ++w;
+            continue;
+        }
         if (MIXED && wall_cull(p.w32[w], rf)) continue;
         wall_exact<EYE>(p.w64[w], w, p, r, h);
     }
@@ -612,6 +660,12 @@ __device__ __forceinline__ HitD closest_hit_bin(const KParams& p, const RayD& r,
     while (wm) {
         const int w = __builtin_ctzll(wm);
         wm &= wm - 1;
+        if (!MIXED && RT_WALL_PAIRS && wm) {
+            const int w1 = __builtin_ctzll(wm);
+            wm &= wm - 1;
+            wall_pair<EYE>(p, w, w1, r, h);
+            continue;
+        }
         if (MIXED && wall_cull(p.w32[w], rf)) continue;
         wall_exact<EYE>(p.w64[w], w, p, r, h);
     }

@@ -79,6 +79,19 @@ def main():
                  first_quarter_dur=round(float(dur[order[: nw // 4]].mean()), 3),
                  last_quarter_dur=round(float(dur[order[-nw // 4:]].mean()), 3))
         print(json.dumps(r), flush=True)
+        cu = (a[:, 2] & 0xffffffff).astype(np.int64)
+        top = np.argsort(-dur)[:12]
+        print(json.dumps({"longest_waves": [
+            dict(tile=[int(w % tx), int(w // tx)], start_us=round(float(t0[w]), 2),
+                 dur_us=round(float(dur[w]), 2), segs=int(segs[w]), hw=int(cu[w])) for w in top]}))
+        # how many of the 1% longest waves share a hardware slot id with another one
+        k = max(1, nw // 100)
+        heavy = np.argsort(-dur)[:k]
+        vals, counts = np.unique(cu[heavy], return_counts=True)
+        print(json.dumps({"heavy_1pct": k, "distinct_hw_ids": int(len(vals)),
+                          "max_per_hw_id": int(counts.max()),
+                          "heavy_start_us_p50": round(float(np.median(t0[heavy])), 2),
+                          "heavy_end_us_p50": round(float(np.median(t1[heavy])), 2)}), flush=True)
         saved[su] = dict(t0=t0.tolist()[:0], dur_map=dur.reshape(ty, tx).round(3).tolist())
     if args.save:
         json.dump(saved, open(args.save, "w"))
