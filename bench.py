@@ -97,8 +97,8 @@ def load_traffic(path: str, workload: str, precision: str):
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawTextHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="c2", choices=sorted(scenes.CONFIGS))
     ap.add_argument("--precision", default="path64", choices=sorted(capi.PRECISIONS))
     ap.add_argument("--mode", default="frames", choices=["frames", "tiled"])
@@ -106,6 +106,9 @@ def main() -> int:
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sweep", action="store_true", help="skip the per-precision kernel sweep")
+    ap.add_argument("--box-cache", type=int, default=0, choices=[0, 1],
+                    help="RT_OPT_BOX_CACHE: reuse the host's per-frame pixel boxes when the "
+                         "camera is unchanged (0 = recompute every frame)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
 
@@ -136,6 +139,7 @@ def main() -> int:
     depth = cfg.depth
 
     rend = capi.Renderer(local)
+    rend.set_option(capi.RT_OPT_BOX_CACHE, args.box_cache)
     rend.set_scene(prims)
     cam = capi.camera_init(**scenes.camera_args(cfg.width, cfg.height))
     W, H = cam.width, cam.height
@@ -293,6 +297,7 @@ def main() -> int:
                 "segments_per_pixel": round(total_segs / px_step, 4),
                 "parallelism": (f"frame-sharded x{world}" if args.mode == "frames"
                                 else f"row-tiled x{world} + gather"),
+                "host_box_cache": bool(args.box_cache),
             },
             "ms_per_frame": round(ms_step / frames_per_step if args.mode == "frames" else ms_step, 4),
             "mpx_per_s": round(px_step * args.steps / elapsed_s / 1e6, 2),

@@ -149,10 +149,14 @@ enum rt_option {
     RT_OPT_ROW_ORDER = 5,             /* 1 (default): tile rows are dispatched centre-out
                                          from the estimated heaviest row (scheduling only);
                                          0 = top to bottom.  Output is identical. */
-    RT_OPT_MIRROR_BINS = 6            /* 1 (default): bounces that follow the same wall
+    RT_OPT_MIRROR_BINS = 6,           /* 1 (default): bounces that follow the same wall
                                          chain across a wave use the boxes of the mirrored
                                          camera (needs RT_OPT_TILE_BINS); 0 = off.  Output
                                          is identical. */
+    RT_OPT_BOX_CACHE = 7              /* 1 (default): a render whose scene, camera, band and
+                                         options equal the previous render's reuses its
+                                         per-frame pixel boxes (host work only); 0 = always
+                                         recompute.  Output is identical. */
 };
 int rt_set_option(rt_ctx* ctx, int32_t option, int64_t value);
 

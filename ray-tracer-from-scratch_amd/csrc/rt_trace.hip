@@ -815,30 +815,42 @@ __device__ __forceinline__ uint64_t tile_keep(const KParams& p, const PrimBox* b
     return box_keep(p, box_load(p, boxes));
 }
 
-/* Bounce k <= mir_depth after a chain of wall hits (rt_device.h "mirror bins"): when
- * every live lane's previous k segments hit the same walls in the same order, the wave's
- * rays are primary rays of the camera mirrored along that chain, whose per-primitive
- * pixel boxes the host provides.  Returns the keep mask, or ~0 when the lanes' paths
- * differ (or a sphere was hit).  st_m: the lane's material-slot stack (valid where
- * alive).  All lanes active; k wave-uniform. */
+/* Bounce k <= mir_depth after chains of wall hits (rt_device.h "mirror bins"): a lane whose
+ * previous k segments hit walls w1..wk has a ray of the camera mirrored along that chain,
+ * so it can only hit primitives whose box for that chain meets the tile.  The wave's keep
+ * mask is the union over the distinct chains its live lanes followed (at most
+ * RT_MIR_CHAINS of them; more, or a sphere anywhere in a chain, returns ~0 = scan all).
+ * st_m: the lane's material-slot stack (valid where alive).  All lanes active; k
+ * wave-uniform. */
+#ifndef RT_MIR_CHAINS
+#define RT_MIR_CHAINS 4
+#endif
 template <int MAXD>
 __device__ __forceinline__ uint64_t mirror_keep(const KParams& p, bool alive, const int* st_m,
                                                 int k) {
-    const uint64_t live = uniform64(__ballot(alive));
-    if (live == 0 || k > p.mir_depth) return ~0ull;
-    const int l0 = __builtin_ctzll(live);
-    int q = 0, off = 0, lvl = 1;
+    uint64_t todo = uniform64(__ballot(alive));
+    if (todo == 0 || k > p.mir_depth) return ~0ull;
+    uint64_t keep = 0;
+    for (int c = 0; c < RT_MIR_CHAINS; ++c) {
+        const int l0 = __builtin_ctzll(todo);
+        bool same = alive;
+        int q = 0, off = 0, lvl = 1;
 #pragma unroll
-    for (int j = 0; j < MIR_MAX_DEPTH && j < MAXD; ++j) {
-        if (j < k) {
-            const int sj = __builtin_amdgcn_readlane(st_m[j], l0);
-            if (sj < p.nS || uniform64(__ballot(alive && st_m[j] != sj)) != 0) return ~0ull;
-            q = q * p.nW + (sj - p.nS);
-            if (j > 0) off += lvl;
-            lvl *= p.nW;
+        for (int j = 0; j < MIR_MAX_DEPTH && j < MAXD; ++j) {
+            if (j < k) {
+                const int sj = __builtin_amdgcn_readlane(st_m[j], l0);
+                if (sj < p.nS) return ~0ull;  // a sphere bounce: no linear mirror
+                same = same && st_m[j] == sj;
+                q = q * p.nW + (sj - p.nS);
+                if (j > 0) off += lvl;
+                lvl *= p.nW;
+            }
         }
+        keep |= tile_keep(p, p.mbox + (off + q) * p.nbox);
+        todo &= ~uniform64(__ballot(same));
+        if (todo == 0) return keep;
     }
-    return tile_keep(p, p.mbox + (off + q) * p.nbox);
+    return ~0ull;
 }
 
 /* find_closest_hit for one segment of every live lane: the wave-culled scan (CULL) or the
@@ -936,6 +948,12 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
             ray_terms(r);
             terms = true;
         }
+#if RT_DIAG
+        if (k >= 1 && __any(alive)) {
+            if (km != ~0ull) DIAG(12);
+            else DIAG(14);
+        }
+#endif
         const HitD h = scan_d<MIXED, CULL>(p, r, alive, k == 0, km != ~0ull, km);
         const bool last = k >= p.depth || k >= MAXD;  // remaining_iterations <= 0 (main.cpp:105)
         if (LAZY && !terms && __any(alive && !last && h.slot >= 0)) {  // a reflection follows

@@ -49,6 +49,7 @@ RT_OPT_EYE_TABLES = 3
 RT_OPT_TILE_BINS = 4
 RT_OPT_ROW_ORDER = 5
 RT_OPT_MIRROR_BINS = 6
+RT_OPT_BOX_CACHE = 7
 
 
 class rt_material(C.Structure):

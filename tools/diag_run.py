@@ -16,6 +16,7 @@ sys.path.insert(0, os.path.join(REPO, "ray-tracer-from-scratch_amd"))
 from rtamd import capi, scenes  # noqa: E402
 
 NAMES = {0: "scan", 2: "sphere_hit_body", 4: "wall_sign_pass", 6: "wall_bounds_body",
+         12: "bounce_scan_binned", 14: "bounce_scan_unbinned",
          8: "shade_nonterminal", 10: "terminal_f32"}
 
 
