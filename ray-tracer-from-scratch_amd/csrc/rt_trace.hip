@@ -823,7 +823,7 @@ __device__ __forceinline__ uint64_t tile_keep(const KParams& p, const PrimBox* b
  * st_m: the lane's material-slot stack (valid where alive).  All lanes active; k
  * wave-uniform. */
 #ifndef RT_MIR_CHAINS
-#define RT_MIR_CHAINS 4
+#define RT_MIR_CHAINS 1  // A/B: 4 chains = the same speed at c2, more SALU
 #endif
 template <int MAXD>
 __device__ __forceinline__ uint64_t mirror_keep(const KParams& p, bool alive, const int* st_m,
