@@ -106,6 +106,9 @@ def main() -> int:
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sweep", action="store_true", help="skip the per-precision kernel sweep")
+    ap.add_argument("--row-feedback", type=int, default=32,
+                    help="RT_OPT_ROW_FEEDBACK: refresh interval (frames) of the measured "
+                         "tile-row dispatch order, 0 = off (scheduling only)")
     ap.add_argument("--box-cache", type=int, default=0, choices=[0, 1],
                     help="RT_OPT_BOX_CACHE: reuse the host's per-frame pixel boxes when the "
                          "camera is unchanged (0 = recompute every frame)")
@@ -140,6 +143,7 @@ def main() -> int:
 
     rend = capi.Renderer(local)
     rend.set_option(capi.RT_OPT_BOX_CACHE, args.box_cache)
+    rend.set_option(capi.RT_OPT_ROW_FEEDBACK, args.row_feedback)
     rend.set_scene(prims)
     cam = capi.camera_init(**scenes.camera_args(cfg.width, cfg.height))
     W, H = cam.width, cam.height
@@ -298,6 +302,7 @@ def main() -> int:
                 "parallelism": (f"frame-sharded x{world}" if args.mode == "frames"
                                 else f"row-tiled x{world} + gather"),
                 "host_box_cache": bool(args.box_cache),
+                "row_feedback": args.row_feedback,
             },
             "ms_per_frame": round(ms_step / frames_per_step if args.mode == "frames" else ms_step, 4),
             "mpx_per_s": round(px_step * args.steps / elapsed_s / 1e6, 2),

@@ -153,12 +153,24 @@ enum rt_option {
                                          chain across a wave use the boxes of the mirrored
                                          camera (needs RT_OPT_TILE_BINS); 0 = off.  Output
                                          is identical. */
-    RT_OPT_BOX_CACHE = 7              /* 1 (default): a render whose scene, camera, band and
+    RT_OPT_BOX_CACHE = 7,             /* 1 (default): a render whose scene, camera, band and
                                          options equal the previous render's reuses its
                                          per-frame pixel boxes (host work only); 0 = always
                                          recompute.  Output is identical. */
+    RT_OPT_ROW_FEEDBACK = 8           /* N > 0 (default 32): every render records each
+                                         tile's cost; every N frames (and at once for a new
+                                         band or scene) a snapshot is copied back behind the
+                                         kernel, and later renders of the same band dispatch
+                                         tile rows heaviest-first by it (scheduling only);
+                                         0 = off.  Output is identical. */
 };
 int rt_set_option(rt_ctx* ctx, int32_t option, int64_t value);
+
+/* Explicit dispatch order of the tile rows (8 pixel rows each): perm is a permutation of
+ * 0..n-1, used by every render whose band has exactly n tile rows, ahead of
+ * RT_OPT_ROW_FEEDBACK; n = 0 clears it.  Scheduling only: output is identical.
+ * RT_ERR_INVALID_ARG if perm is not a permutation or n > 1024. */
+int rt_set_row_order(rt_ctx* ctx, const int16_t* perm, int32_t n);
 
 /* ---- frame operators (replace rt_scene, main.cpp:124-139) --------------- */
 /* Render rows [row0, row0+nrows) of the frame into caller-owned HOST memory `out`

@@ -41,6 +41,29 @@ struct rt_ctx {
     bool tile_bins = true;   // RT_OPT_TILE_BINS
     bool row_order = true;   // RT_OPT_ROW_ORDER
     bool mirror_bins = true; // RT_OPT_MIRROR_BINS
+    std::vector<int16_t> row_perm;  // rt_set_row_order: explicit tile-row dispatch order
+    // Row feedback (RT_OPT_ROW_FEEDBACK): every render records each wave's cost
+    // (KParams::tile_cost); every `feedback` frames a snapshot is copied to pinned host
+    // memory behind the kernel and, once it has landed, the tile rows are ordered by their
+    // most expensive tile (heaviest first) for the following renders of the same band.
+    // Only the dispatch order changes: every tile is traced once per frame either way.
+    int feedback = 32;             // refresh interval in frames, 0 = off
+    uint16_t* d_cost = nullptr;    // device, d_cost_cap entries
+    uint16_t* h_cost = nullptr;    // pinned host snapshot
+    size_t d_cost_cap = 0;
+    hipEvent_t ev_cost = nullptr;  // snapshot landed
+    bool cost_pending = false;
+    struct Band {
+        int32_t W = -1, row0 = -1, nrows = -1;
+        unsigned long long scene_gen = 0;
+        bool operator==(const Band& o) const {
+            return W == o.W && row0 == o.row0 && nrows == o.nrows && scene_gen == o.scene_gen;
+        }
+    };
+    Band cost_band;                // band of the pending snapshot
+    Band fb_band;                  // band fb_perm was computed for
+    std::vector<int16_t> fb_perm;
+    int since_snapshot = 0;
     // the per-frame boxes depend only on the scene, the camera, the row band and the
     // options: a render with the same inputs as the previous one reuses them (the host
     // part of a frame is ~60 us with mirror chains, more than the kernel at c2)
@@ -707,6 +730,9 @@ int rt_ctx_create(int device, rt_ctx** out) {
         }
         if ((e = hipEventCreate(&ctx->ev0)) != hipSuccess) { st = hip_fail(ctx, e, "hipEventCreate"); break; }
         if ((e = hipEventCreate(&ctx->ev1)) != hipSuccess) { st = hip_fail(ctx, e, "hipEventCreate"); break; }
+        if ((e = hipEventCreateWithFlags(&ctx->ev_cost, hipEventDisableTiming)) != hipSuccess) {
+            st = hip_fail(ctx, e, "hipEventCreate"); break;
+        }
         if ((e = hipMalloc(&ctx->d_segs, sizeof(unsigned long long))) != hipSuccess) {
             st = hip_fail(ctx, e, "hipMalloc(segs)"); break;
         }
@@ -726,6 +752,10 @@ int rt_ctx_destroy(rt_ctx* ctx) {
     if (ctx->d_scene) (void)hipFree(ctx->d_scene);
     if (ctx->d_out) (void)hipFree(ctx->d_out);
     if (ctx->d_segs) (void)hipFree(ctx->d_segs);
+    if (ctx->ev_cost) (void)hipEventSynchronize(ctx->ev_cost);
+    if (ctx->d_cost) (void)hipFree(ctx->d_cost);
+    if (ctx->h_cost) (void)hipHostFree(ctx->h_cost);
+    if (ctx->ev_cost) (void)hipEventDestroy(ctx->ev_cost);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -810,6 +840,14 @@ int rt_set_option(rt_ctx* ctx, int32_t option, int64_t value) {
             if (value != 0 && value != 1) return RT_ERR_INVALID_ARG;
             ctx->row_order = value == 1;
             return RT_OK;
+        case RT_OPT_ROW_FEEDBACK:
+            if (value < 0 || value > 1000000) return RT_ERR_INVALID_ARG;
+            ctx->feedback = (int)value;
+            if (value == 0) {
+                ctx->fb_perm.clear();
+                ctx->fb_band = rt_ctx::Band{};
+            }
+            return RT_OK;
         default:
             return RT_ERR_INVALID_ARG;
     }
@@ -828,6 +866,96 @@ int rt_selftest(rt_ctx* ctx, int32_t test, uint64_t n, uint64_t seed, uint64_t* 
     return RT_OK;
 }
 
+/* Explicit tile-row dispatch order (a permutation of 0 .. n-1), used by renders whose grid
+ * has exactly n tile rows; n == 0 clears it. */
+int rt_set_row_order(rt_ctx* ctx, const int16_t* perm, int32_t n) {
+    if (!ctx || n < 0 || n > rt::ROW_PERM_MAX || (n > 0 && !perm)) return RT_ERR_INVALID_ARG;
+    std::vector<char> seen(n, 0);
+    for (int j = 0; j < n; j++) {
+        if (perm[j] < 0 || perm[j] >= n || seen[perm[j]]) return RT_ERR_INVALID_ARG;
+        seen[perm[j]] = 1;
+    }
+    ctx->row_perm.assign(perm, perm + n);
+    return RT_OK;
+}
+
+/* Tile rows ordered by their most expensive wave (heaviest first; ties keep the lower
+ * row), from a cost snapshot of gy rows x per_row waves. */
+static void order_rows(const uint16_t* cost, int gy, int per_row, std::vector<int16_t>& perm) {
+    std::vector<uint32_t> mx(gy, 0);
+    for (int r = 0; r < gy; r++) {
+        const uint16_t* c = cost + (size_t)r * per_row;
+        uint32_t m = 0;
+        for (int k = 0; k < per_row; k++) m = std::max<uint32_t>(m, c[k]);
+        mx[r] = m;
+    }
+    perm.resize(gy);
+    for (int r = 0; r < gy; r++) perm[r] = (int16_t)r;
+    std::stable_sort(perm.begin(), perm.end(), [&](int16_t a, int16_t b) { return mx[a] > mx[b]; });
+}
+
+/* Before a launch: the row order (explicit, else the feedback's for this band) and the
+ * cost buffer.  Returns an rt_status. */
+static int prepare_rows(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nrows,
+                        hipStream_t st, rt::KParams& p) {
+    const int gy = (nrows + rt::TILE_H - 1) / rt::TILE_H;
+    const int per_row = ((cam->width + rt::TILE_W - 1) / rt::TILE_W) * (rt::BLOCK / 64);
+    const rt_ctx::Band band{cam->width, row0, nrows, ctx->scene_gen};
+    if (ctx->cost_pending && hipEventQuery(ctx->ev_cost) == hipSuccess) {
+        ctx->cost_pending = false;
+        const rt_ctx::Band& b = ctx->cost_band;
+        order_rows(ctx->h_cost, (b.nrows + rt::TILE_H - 1) / rt::TILE_H,
+                   ((b.W + rt::TILE_W - 1) / rt::TILE_W) * (rt::BLOCK / 64), ctx->fb_perm);
+        ctx->fb_band = b;
+    }
+    const std::vector<int16_t>* perm = nullptr;
+    if (!ctx->row_perm.empty()) perm = &ctx->row_perm;
+    else if (ctx->feedback > 0 && ctx->fb_band == band && !ctx->fb_perm.empty()) perm = &ctx->fb_perm;
+    if (perm && (int)perm->size() == gy && gy <= rt::ROW_PERM_MAX) {
+        p.row_perm_n = gy;
+        std::memcpy(p.row_perm, perm->data(), gy * sizeof(int16_t));
+    }
+    // sample this frame's costs when a snapshot is due (snapshot_costs copies them)
+    p.tile_cost = nullptr;
+    if (ctx->feedback <= 0 || !ctx->row_perm.empty() || gy > rt::ROW_PERM_MAX || ctx->cost_pending)
+        return RT_OK;
+    if (++ctx->since_snapshot < ctx->feedback && ctx->fb_band == band) return RT_OK;
+    const size_t need = (size_t)gy * per_row;
+    if (need > ctx->d_cost_cap) {
+        // grow (rare): nothing in flight may still use the old buffers
+        RT_HIP(ctx, hipStreamSynchronize(st));
+        if (ctx->cost_pending) RT_HIP(ctx, hipEventSynchronize(ctx->ev_cost));
+        ctx->cost_pending = false;
+        if (ctx->d_cost) RT_HIP(ctx, hipFree(ctx->d_cost));
+        if (ctx->h_cost) RT_HIP(ctx, hipHostFree(ctx->h_cost));
+        ctx->d_cost = nullptr;
+        ctx->h_cost = nullptr;
+        ctx->d_cost_cap = 0;
+        RT_HIP(ctx, hipMalloc(&ctx->d_cost, need * sizeof(uint16_t)));
+        RT_HIP(ctx, hipHostMalloc(&ctx->h_cost, need * sizeof(uint16_t), hipHostMallocDefault));
+        ctx->d_cost_cap = need;
+    }
+    p.tile_cost = ctx->d_cost;
+    return RT_OK;
+}
+
+/* After a launch that sampled its costs (every `feedback` frames, or at once for a band the
+ * order does not cover yet): copy them back behind the kernel. */
+static int snapshot_costs(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nrows,
+                          hipStream_t st, const rt::KParams& p) {
+    if (!p.tile_cost) return RT_OK;
+    const rt_ctx::Band band{cam->width, row0, nrows, ctx->scene_gen};
+    const int gy = (nrows + rt::TILE_H - 1) / rt::TILE_H;
+    const size_t n = (size_t)gy * ((cam->width + rt::TILE_W - 1) / rt::TILE_W) * (rt::BLOCK / 64);
+    RT_HIP(ctx, hipMemcpyAsync(ctx->h_cost, ctx->d_cost, n * sizeof(uint16_t),
+                               hipMemcpyDeviceToHost, st));
+    RT_HIP(ctx, hipEventRecord(ctx->ev_cost, st));
+    ctx->cost_pending = true;
+    ctx->cost_band = band;
+    ctx->since_snapshot = 0;
+    return RT_OK;
+}
+
 int rt_render_device(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nrows,
                      int32_t depth, int32_t precision, uint32_t flags, int32_t out_format,
                      void* d_out, uint64_t* d_segments, void* stream) {
@@ -837,9 +965,12 @@ int rt_render_device(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nr
     rt::KParams p = make_params(ctx, cam, row0, nrows, depth, flags, out_format, d_out,
                                 reinterpret_cast<unsigned long long*>(d_segments));
     void* s = stream ? stream : static_cast<void*>(ctx->stream);
+    hipStream_t hs = static_cast<hipStream_t>(s);
+    st = prepare_rows(ctx, cam, row0, nrows, hs, p);
+    if (st != RT_OK) return st;
     const int e = rt::launch_trace(p, precision, s);
     if (e != (int)hipSuccess) return hip_fail(ctx, (hipError_t)e, "launch k_trace");
-    return RT_OK;
+    return snapshot_costs(ctx, cam, row0, nrows, hs, p);
 }
 
 int rt_render(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nrows, int32_t depth,
@@ -862,10 +993,14 @@ int rt_render(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nrows, in
     if (segs) RT_HIP(ctx, hipMemsetAsync(segs, 0, sizeof *segs, ctx->stream));
     rt::KParams p = make_params(ctx, cam, row0, nrows, depth, flags, out_format,
                                 ctx->d_out, segs);
+    st = prepare_rows(ctx, cam, row0, nrows, ctx->stream, p);
+    if (st != RT_OK) return st;
     RT_HIP(ctx, hipEventRecord(ctx->ev0, ctx->stream));
     const int e = rt::launch_trace(p, precision, ctx->stream);
     if (e != (int)hipSuccess) return hip_fail(ctx, (hipError_t)e, "launch k_trace");
     RT_HIP(ctx, hipEventRecord(ctx->ev1, ctx->stream));
+    st = snapshot_costs(ctx, cam, row0, nrows, ctx->stream, p);
+    if (st != RT_OK) return st;
     if (bytes > 0)
         RT_HIP(ctx, hipMemcpyAsync(out, ctx->d_out, bytes, hipMemcpyDeviceToHost, ctx->stream));
     unsigned long long hsegs = 0;

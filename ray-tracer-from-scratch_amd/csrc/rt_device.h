@@ -113,6 +113,13 @@ struct PrimBox {
     int16_t x0, x1, i0, i1;  // inclusive pixel box (frame rows); x0 > x1 = never hit
 };
 
+// Tile-row dispatch order given explicitly (up to ROW_PERM_MAX tile rows, 8-row tiles:
+// 8192 pixel rows).
+#ifndef RT_ROW_PERM_MAX
+#define RT_ROW_PERM_MAX 1024
+#endif
+constexpr int ROW_PERM_MAX = RT_ROW_PERM_MAX;
+
 struct KParams {
     const SphG32* s32;
     const SphG64* s64;
@@ -136,6 +143,10 @@ struct KParams {
     unsigned long long* stats;  // diagnostic counters, may be null (rt_set_option)
     int32_t nbox;               // primitives with a PrimBox (nS + nW), 0 = tile bins off
     int32_t row_center;         // tile row dispatched first (rt_trace.hip tile_row), -1 = off
+    uint16_t* tile_cost;        // per wave (workgroup row-major over the frame's tiles, then
+                                // wave): shader cycles / 32, saturated; null = not recorded
+    int32_t row_perm_n;         // tile rows in row_perm (== the grid's rows), 0 = unused
+    int16_t row_perm[ROW_PERM_MAX];  // dispatch order of tile rows (rt_trace.hip tile_row)
     PrimBox box[BIN_MAX_PRIMS]; // material-slot order: spheres, then walls
     int32_t mir_depth;          // wall-sequence levels with mirror boxes (0 = off)
     int32_t pad_mir;

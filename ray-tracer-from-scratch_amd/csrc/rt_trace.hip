@@ -43,6 +43,7 @@
 #include <float.h>
 #include <math.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "rt_device.h"
@@ -73,6 +74,13 @@
 #endif
 #ifndef RT_DIAG            // diagnostic build: count wave/lane entries of branch bodies
 #define RT_DIAG 0          // into g_diag (rt_diag_read); never on in the product
+#endif
+#ifndef RT_STAMP
+#define RT_STAMP 0  // 1 in rt_trace_stamp.hip: the same kernels, recording each wave's cost
+#endif
+#if RT_DIAG && RT_STAMP
+#undef RT_DIAG
+#define RT_DIAG 0
 #endif
 #if RT_DIAG
 __device__ unsigned long long g_diag[16];
@@ -106,6 +114,14 @@ __device__ unsigned long long g_diag[16];
 #endif
 
 namespace rt {
+// The kernels are built twice, as rt::kno (this file) and rt::kst (rt_trace_stamp.hip, for
+// the frames whose costs the host samples for the dispatch order, rt_capi.cpp): a wave-start
+// s_memtime costs ~15% at c2 wherever it sits (tools/ab.py), so the plain kernels have none.
+#if RT_STAMP
+namespace kst {
+#else
+namespace kno {
+#endif
 
 /* ------------------------------------------------------------------------ */
 /* fp64 vector math, vec.cpp:3-57 (this TU: -ffp-contract=off)               */
@@ -776,16 +792,21 @@ __device__ __forceinline__ f3 tof(d3 v) { return F3((float)v.x, (float)v.y, (flo
  * light one: the dispatcher goes row by row, so rows are visited centre-out from the
  * host's estimate of the heaviest row (KParams::row_center, rt_capi.cpp) — heavy work
  * first, the cheap rows fill in around it.  Identity when row_center < 0. */
-__device__ __forceinline__ int tile_row(const KParams& p) {
-    const int j = blockIdx.y, c = p.row_center, n = gridDim.y;
-    if (c < 0 || c >= n) return j;
+__device__ __forceinline__ int tile_row(const KParams& p, int j, int n) {
+    // branch-free (scalar selects), so that its kernel-argument loads — including the dword
+    // holding entry j of an explicit order (a 16-bit load would be a vector load) — issue in
+    // the wave's first batch instead of one dependent round trip after another
+    const int c = p.row_center, rpn = p.row_perm_n;
+    const uint32_t w = reinterpret_cast<const uint32_t*>(p.row_perm)[min(j >> 1, ROW_PERM_MAX / 2 - 1)];
     const int L = min(c, n - 1 - c);  // rows c-L .. c+L alternate
-    if (j <= 2 * L) {
-        const int d = (j + 1) >> 1;
-        return (j & 1) ? c + d : c - d;
-    }
+    const int d = (j + 1) >> 1;
+    const int alt = (j & 1) ? c + d : c - d;
     const int e = j - 2 * L;  // one side is exhausted: continue on the other
-    return (c - L == 0) ? c + L + e : c - L - e;
+    const int rest = (c - L == 0) ? c + L + e : c - L - e;
+    int t = j <= 2 * L ? alt : rest;
+    t = (c < 0 || c >= n) ? j : t;
+    const int pj = (int16_t)((j & 1) ? (w >> 16) : (w & 0xffff));
+    return rpn == n ? pj : t;
 }
 
 __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
@@ -802,17 +823,25 @@ __device__ __forceinline__ uint64_t box_load(const KParams& p, const PrimBox* bo
     const uint64_t v = *reinterpret_cast<const uint64_t*>(boxes + (l < p.nbox ? l : 0));
     return l < p.nbox ? v : 0x80007fff80007fffull;  // x0 = i0 = 32767 > x1 = i1: never meets
 }
-__device__ __forceinline__ uint64_t box_keep(const KParams& p, uint64_t raw) {
-    const int wave = threadIdx.x >> 6;
-    const int tx0 = blockIdx.x * TILE_W + (TILE_W > 8 ? (wave & 1) * 8 : 0);
-    const int ty0 = p.row0 + tile_row(p) * TILE_H + (TILE_H > 8 ? (wave >> 1) * 8 : 0);
+/* Pixel origin of the wave's 8x8 tile from a lane's own pixel (every wave covers an 8x8
+ * square, lane = 8 * row + column): wave-uniform, independent of how tiles map to
+ * workgroups. */
+struct TileO {
+    int x0, y0;
+};
+__device__ __forceinline__ TileO tile_origin(int x, int i) {
+    const int lane = threadIdx.x & 63;
+    return {__builtin_amdgcn_readfirstlane(x - (lane & 7)),
+            __builtin_amdgcn_readfirstlane(i - (lane >> 3))};
+}
+__device__ __forceinline__ uint64_t box_keep(uint64_t raw, TileO t) {
     const int x0 = (int16_t)(raw & 0xffff), x1 = (int16_t)((raw >> 16) & 0xffff);
     const int i0 = (int16_t)((raw >> 32) & 0xffff), i1 = (int16_t)(raw >> 48);
-    const bool hit = (x0 <= tx0 + 7) & (x1 >= tx0) & (i0 <= ty0 + 7) & (i1 >= ty0);
+    const bool hit = (x0 <= t.x0 + 7) & (x1 >= t.x0) & (i0 <= t.y0 + 7) & (i1 >= t.y0);
     return uniform64(__ballot(hit));
 }
-__device__ __forceinline__ uint64_t tile_keep(const KParams& p, const PrimBox* boxes) {
-    return box_keep(p, box_load(p, boxes));
+__device__ __forceinline__ uint64_t tile_keep(const KParams& p, const PrimBox* boxes, TileO t) {
+    return box_keep(box_load(p, boxes), t);
 }
 
 /* Bounce k <= mir_depth after chains of wall hits (rt_device.h "mirror bins"): a lane whose
@@ -827,7 +856,7 @@ __device__ __forceinline__ uint64_t tile_keep(const KParams& p, const PrimBox* b
 #endif
 template <int MAXD>
 __device__ __forceinline__ uint64_t mirror_keep(const KParams& p, bool alive, const int* st_m,
-                                                int k) {
+                                                int k, TileO t) {
     uint64_t todo = uniform64(__ballot(alive));
     if (todo == 0 || k > p.mir_depth) return ~0ull;
     uint64_t keep = 0;
@@ -846,7 +875,7 @@ __device__ __forceinline__ uint64_t mirror_keep(const KParams& p, bool alive, co
                 lvl *= p.nW;
             }
         }
-        keep |= tile_keep(p, p.mbox + (off + q) * p.nbox);
+        keep |= tile_keep(p, p.mbox + (off + q) * p.nbox, t);
         todo &= ~uniform64(__ballot(same));
         if (todo == 0) return keep;
     }
@@ -908,7 +937,7 @@ __device__ __forceinline__ HitD scan_d(const KParams& p, const RayD& r, bool ali
  * MIXED, the parity modes); otherwise in fp32 (PATH64). */
 template <bool MIXED, bool COLOR64, bool SUN, bool INT_EXP, bool CULL, int MAXD>
 __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool alive,
-                                            int& segs) {
+                                            int& segs, uint64_t& t_start) {
     using CT = typename std::conditional<COLOR64, double, float>::type;
     const d3 cpos = ld3(p.pos);
     const d3 pc = (ld3(p.tl) + ld3(p.dx) * (double)x) + ld3(p.dy) * (double)i;  // main.cpp:132
@@ -919,8 +948,12 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
     RayD r = LAZY ? make_ray_lazy(cpos, cpos - pc) : make_ray(cpos, cpos - pc);
     bool terms = !LAZY;
     constexpr bool sun = SUN;
+    // the wave's start stamp for the dispatch-order feedback (stamped build only): here,
+    // between ray generation and the box compare's wait on its load
+    t_start = RT_STAMP ? __builtin_amdgcn_s_memtime() : 0;
     if (RT_BOX_SCHED_BARRIER) __builtin_amdgcn_sched_barrier(0);  // compare after ray gen
-    uint64_t keep = CULL ? ~0ull : box_keep(p, braw);  // all lanes active
+    const TileO tile = tile_origin(x, i);
+    uint64_t keep = CULL ? ~0ull : box_keep(braw, tile);  // all lanes active
     if (p.nbox == 0) keep = ~0ull;
     const uint64_t smask = p.nS >= 64 ? ~0ull : (1ull << p.nS) - 1;
 
@@ -943,7 +976,7 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
         // reflected off one wall (both wave-uniform)
         uint64_t km = ~0ull;
         if (!CULL && k == 0 && p.nbox > 0) km = keep;
-        if (!CULL && k >= 1 && k <= p.mir_depth) km = mirror_keep<MAXD>(p, alive, st_m, k);
+        if (!CULL && k >= 1 && k <= p.mir_depth) km = mirror_keep<MAXD>(p, alive, st_m, k, tile);
         if (LAZY && !terms && (km & smask) != 0) {  // a sphere may be tested
             ray_terms(r);
             terms = true;
@@ -1156,7 +1189,7 @@ __device__ __forceinline__ void walls_f(const KParams& p, f3 o, f3 d, float& bes
 
 template <bool SUN, bool CULL, int MAXD>
 __device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, bool alive,
-                                            int& segs) {
+                                            int& segs, uint64_t& t_start) {
     const d3 pcd = (ld3(p.tl) + ld3(p.dx) * (double)x) + ld3(p.dy) * (double)i;
     const d3 dd = ld3(p.pos) - pcd;
     f3 o = F3((float)p.pos[0], (float)p.pos[1], (float)p.pos[2]);
@@ -1168,7 +1201,9 @@ __device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, bool
     int st_m[MAXD];
     int n = 0;
     f3 c = F3(0.f, 0.f, 0.f);
-    const uint64_t keep = (!CULL && p.nbox > 0) ? tile_keep(p, p.box) : ~0ull;  // all lanes active
+    t_start = RT_STAMP ? __builtin_amdgcn_s_memtime() : 0;  // see trace_pixel_d
+    const TileO tile = tile_origin(x, i);
+    const uint64_t keep = (!CULL && p.nbox > 0) ? tile_keep(p, p.box, tile) : ~0ull;
     int kend = 0;  // wave-uniform: bounce iterations run (every lane's n <= kend)
     for (int k = 0;; ++k) {
         if (!__any(alive)) {
@@ -1185,7 +1220,7 @@ __device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, bool
         // reflected off one wall (both wave-uniform)
         uint64_t km = ~0ull;
         if (!CULL && k == 0 && p.nbox > 0) km = keep;
-        if (!CULL && k >= 1 && k <= p.mir_depth) km = mirror_keep<MAXD>(p, alive, st_m, k);
+        if (!CULL && k >= 1 && k <= p.mir_depth) km = mirror_keep<MAXD>(p, alive, st_m, k, tile);
         const bool binned = km != ~0ull;
         if (!CULL && binned) {
             // kept spheres in index order, kept walls
@@ -1355,41 +1390,55 @@ constexpr int waves_per_eu() {
     return w < 2 ? 2 : w;
 }
 
+/* One tile per wave: tile column bx, tile row trow (after the row order), gx tile columns. */
 template <int PREC, bool SUN, bool INT_EXP, bool CULL, int MAXD>
-__global__ void __launch_bounds__(BLOCK)
-__attribute__((amdgpu_waves_per_eu(waves_per_eu<PREC, SUN, INT_EXP, CULL, MAXD>(), 8)))
-k_trace(KParams p) {
+__device__ __forceinline__ void trace_tile(const KParams& p, int bx, int trow, int gx) {
 #if RT_WAVE_TIMES
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
 #endif
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    const int x = blockIdx.x * TILE_W + (TILE_W > 8 ? (wave & 1) * 8 : 0) + (lane & 7);
-    const int r = tile_row(p) * TILE_H + (TILE_H > 8 ? (wave >> 1) * 8 : 0) + (lane >> 3);
+    const int x = bx * TILE_W + (TILE_W > 8 ? (wave & 1) * 8 : 0) + (lane & 7);
+    const int r = trow * TILE_H + (TILE_H > 8 ? (wave >> 1) * 8 : 0) + (lane >> 3);
     const bool valid = x < p.W && r < p.nrows;
+    uint64_t t_tile = 0;  // the wave's start stamp (taken inside trace_pixel_*)
     const int i = p.row0 + r;
     int segs = 0;
     // every lane runs the (converged) bounce loop; only valid lanes trace and store
     if (PREC == PREC_F32) {
-        const f3 c = trace_pixel_f<SUN, CULL, MAXD>(p, x, i, valid, segs);
+        const f3 c = trace_pixel_f<SUN, CULL, MAXD>(p, x, i, valid, segs, t_tile);
         if (valid) store_pixel(p, r, x, c.x, c.y, c.z);
     } else {
         const d3 c =
             trace_pixel_d<PREC == PREC_MIXED, PREC != PREC_PATH64, SUN, INT_EXP, CULL, MAXD>(
-                p, x, i, valid, segs);
+                p, x, i, valid, segs, t_tile);
         if (valid) store_pixel(p, r, x, c.x, c.y, c.z);
     }
     count_segments(p, segs);
+    if (RT_STAMP && lane == 0) {
+        // this tile's cost for the host's next tile-row order (rt_capi.cpp row feedback)
+        const uint64_t c = (__builtin_amdgcn_s_memtime() - t_tile) >> 5;
+        p.tile_cost[((size_t)trow * gx + bx) * (BLOCK / 64) + wave] = (uint16_t)(c < 65535 ? c : 65535);
+    }
 #if RT_WAVE_TIMES
     // diagnostic build: per wave {start, end, segments << 32 | CU id} (100 MHz clock)
     for (int off = 32; off > 0; off >>= 1) segs += __shfl_xor(segs, off, 64);
     if (p.stats != nullptr && lane == 0) {
-        const size_t wid = ((size_t)tile_row(p) * gridDim.x + blockIdx.x) * (BLOCK / 64) + wave;
+        const size_t wid = ((size_t)trow * gx + bx) * (BLOCK / 64) + wave;
         p.stats[3 * wid] = t_start;
         p.stats[3 * wid + 1] = __builtin_amdgcn_s_memrealtime();
         p.stats[3 * wid + 2] = ((unsigned long long)segs << 32) | (unsigned)__smid();
     }
 #endif
+}
+
+
+template <int PREC, bool SUN, bool INT_EXP, bool CULL, int MAXD>
+__global__ void __launch_bounds__(BLOCK)
+__attribute__((amdgpu_waves_per_eu(waves_per_eu<PREC, SUN, INT_EXP, CULL, MAXD>(), 8)))
+k_trace(KParams p) {
+    trace_tile<PREC, SUN, INT_EXP, CULL, MAXD>(p, blockIdx.x, tile_row(p, blockIdx.y, gridDim.y),
+                                               gridDim.x);
 }
 
 template <int PREC, bool SUN, bool INT_EXP, bool CULL>
@@ -1427,9 +1476,9 @@ static hipError_t launch_prec(const KParams& p, dim3 grid, hipStream_t st) {
     }
 }
 
-int max_depth() { return MAXD_LARGE; }
+int max_depth_ns() { return MAXD_LARGE; }
 
-#if RT_DIAG
+#if RT_DIAG && !RT_STAMP
 extern "C" int rt_diag_read(unsigned long long* out16) {
     const int e = (int)hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_diag), sizeof g_diag);
     unsigned long long z[16] = {0};
@@ -1438,7 +1487,7 @@ extern "C" int rt_diag_read(unsigned long long* out16) {
 }
 #endif
 
-int launch_trace(const KParams& p, int prec, void* stream) {
+int launch_trace_ns(const KParams& p, int prec, void* stream) {
     if (p.W <= 0 || p.nrows <= 0) return (int)hipSuccess;
     const dim3 grid((p.W + TILE_W - 1) / TILE_W, (p.nrows + TILE_H - 1) / TILE_H);
     hipStream_t st = static_cast<hipStream_t>(stream);
@@ -1451,6 +1500,7 @@ int launch_trace(const KParams& p, int prec, void* stream) {
     }
 }
 
+#if !RT_STAMP
 /* ------------------------------------------------------------------------ */
 /* self-test of the exact helpers (rt_selftest)                              */
 /* ------------------------------------------------------------------------ */
@@ -1499,11 +1549,31 @@ __global__ void k_selftest(int which, uint64_t n, uint64_t seed, unsigned long l
     if ((threadIdx.x & 63) == 0 && nbad) atomicAdd(bad, nbad);
 }
 
-int launch_selftest(int which, uint64_t n, uint64_t seed, unsigned long long* d_bad,
-                    void* stream) {
+int launch_selftest_ns(int which, uint64_t n, uint64_t seed, unsigned long long* d_bad,
+                       void* stream) {
     hipLaunchKernelGGL(k_selftest, dim3(1024), dim3(256), 0, static_cast<hipStream_t>(stream),
                        which, n, seed, d_bad);
     return (int)hipGetLastError();
 }
+#endif  // !RT_STAMP
+
+}  // namespace kno / kst
+
+#if RT_STAMP
+int launch_trace_stamped(const KParams& p, int prec, void* stream) {
+    return kst::launch_trace_ns(p, prec, stream);
+}
+#else
+int launch_trace_stamped(const KParams& p, int prec, void* stream);  // rt_trace_stamp.hip
+int launch_trace(const KParams& p, int prec, void* stream) {
+    return p.tile_cost != nullptr ? launch_trace_stamped(p, prec, stream)
+                                  : kno::launch_trace_ns(p, prec, stream);
+}
+int max_depth() { return kno::max_depth_ns(); }
+int launch_selftest(int which, uint64_t n, uint64_t seed, unsigned long long* d_bad,
+                    void* stream) {
+    return kno::launch_selftest_ns(which, n, seed, d_bad, stream);
+}
+#endif
 
 }  // namespace rt

@@ -50,6 +50,7 @@ RT_OPT_TILE_BINS = 4
 RT_OPT_ROW_ORDER = 5
 RT_OPT_MIRROR_BINS = 6
 RT_OPT_BOX_CACHE = 7
+RT_OPT_ROW_FEEDBACK = 8
 
 
 class rt_material(C.Structure):
@@ -118,6 +119,7 @@ SIGNATURES = [
       C.POINTER(C.c_int16), C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     ("rt_selftest", C.c_int, [C.c_void_p, C.c_int32, C.c_uint64, C.c_uint64,
                               C.POINTER(C.c_uint64)]),
+    ("rt_set_row_order", C.c_int, [C.c_void_p, C.POINTER(C.c_int16), C.c_int32]),
 ]
 
 _lib = None
@@ -248,6 +250,12 @@ class Renderer:
 
     def set_option(self, option: int, value: int) -> None:
         check(self.lib.rt_set_option(self.ctx, option, value), self.ctx)
+
+    def set_row_order(self, perm) -> None:
+        """rt_set_row_order: explicit tile-row dispatch order (None or [] clears it)."""
+        perm = list(perm or [])
+        arr = (C.c_int16 * max(1, len(perm)))(*perm)
+        check(self.lib.rt_set_row_order(self.ctx, arr if perm else None, len(perm)), self.ctx)
 
     def selftest(self, test: int, n: int, seed: int = 1) -> int:
         bad = C.c_uint64()

@@ -41,6 +41,8 @@ def main():
     ap.add_argument("--precisions", default="f64,path64,f32")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--opt", action="append", default=[],
+                    help="NAME=VALUE: rt_set_option(RT_OPT_NAME) on every build that knows it")
     args = ap.parse_args()
     import torch
     dev = torch.device("cuda", 0)
@@ -48,6 +50,11 @@ def main():
     libs = {"a": Lib(args.a), "b": Lib(args.b)}
     for k, path in zip("cdefgh", [x for x in args.more.split(",") if x]):
         libs[k] = Lib(path)
+    for o in args.opt:
+        name, val = o.split("=")
+        for L in libs.values():
+            # an older build rejects an option it does not know: leave it at its default
+            L.lib.rt_set_option(L.ctx, getattr(capi, "RT_OPT_" + name), int(val))
     for cname in args.configs.split(","):
         cfg = scenes.CONFIGS[cname]
         prims = scenes.to_prims(cfg.scene())
@@ -70,6 +77,17 @@ def main():
                     torch.cuda.synchronize()
                     t[k].append(e0.elapsed_time(e1) / args.reps)
             r = {"config": cname, "precision": pname}
+            # same pixels from every build (max |delta| against build a)
+            imgs = {}
+            for k, L in libs.items():
+                o = torch.full_like(out, -1.0)
+                torch.cuda.synchronize()  # the fill is on torch's stream, the launch on `stream`
+                L.launch(cam, cfg.depth, o.data_ptr(), prec, stream.cuda_stream)
+                torch.cuda.synchronize()
+                imgs[k] = o
+            for k in libs:
+                if k != "a":
+                    r[k + "_maxdiff"] = float((imgs[k] - imgs["a"]).abs().max())
             for k in libs:
                 r[k + "_ms"] = round(min(t[k]), 4)
             for k in libs:

@@ -77,7 +77,13 @@ def main():
                  wave_us_sum_over_span=round(dur.sum() / span, 1),
                  dur_vs_segs_corr=round(float(np.corrcoef(dur, segs)[0, 1]), 3),
                  first_quarter_dur=round(float(dur[order[: nw // 4]].mean()), 3),
-                 last_quarter_dur=round(float(dur[order[-nw // 4:]].mean()), 3))
+                 last_quarter_dur=round(float(dur[order[-nw // 4:]].mean()), 3),
+                 starts_per_us_by_decile=[round(float(((t0 >= a0) & (t0 < a0 + span / 10)).sum()
+                                                      / (span / 10)), 1)
+                                          for a0 in np.arange(10) * span / 10],
+                 dur_mean_by_start_decile=[round(float(dur[(t0 >= a0) & (t0 < a0 + span / 10)]
+                                                       .mean()), 2) if ((t0 >= a0) & (t0 < a0 + span / 10)).any() else None
+                                           for a0 in np.arange(10) * span / 10])
         print(json.dumps(r), flush=True)
         cu = (a[:, 2] & 0xffffffff).astype(np.int64)
         top = np.argsort(-dur)[:12]
@@ -92,7 +98,8 @@ def main():
                           "max_per_hw_id": int(counts.max()),
                           "heavy_start_us_p50": round(float(np.median(t0[heavy])), 2),
                           "heavy_end_us_p50": round(float(np.median(t1[heavy])), 2)}), flush=True)
-        saved[su] = dict(t0=t0.tolist()[:0], dur_map=dur.reshape(ty, tx).round(3).tolist())
+        saved[su] = dict(tx=tx, ty=ty, t0=t0.round(3).tolist(), t1=t1.round(3).tolist(), segs=segs.tolist(),
+                         hw=cu.tolist())
     if args.save:
         json.dump(saved, open(args.save, "w"))
     lib.rt_ctx_destroy(h)
