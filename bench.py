@@ -263,6 +263,38 @@ def main() -> int:
                        "parity": "sun term is build-defined (constants main.cpp:18-19, unused "
                                  "by the reference): pinned to the oracle, not the reference"}
 
+    moving = None
+    if rank == 0 and not args.no_sweep and args.mode == "frames":
+        # the measured tile-row order on a camera that moves every frame (a fly-through of
+        # 200 frames, 0.01 scene units per frame toward the scene — rays travel toward +x,
+        # main.cpp:133): the order is refreshed every RT_OPT_ROW_FEEDBACK frames, so it
+        # lags the view; per-frame ms with the feedback on and off (kernel stream time)
+        ca = scenes.camera_args(W, H)
+        cams = []
+        for f in range(200):
+            dx = 0.01 * f
+            a = dict(ca)
+            a["position"] = (ca["position"][0] + dx, ca["position"][1], ca["position"][2])
+            a["lookat"] = (ca["lookat"][0] + dx, ca["lookat"][1], ca["lookat"][2])
+            cams.append(capi.camera_init(**a))
+        moving = {"frames": len(cams), "step": "0.01 units/frame along +x"}
+        for fb in (0, args.row_feedback):
+            rend.set_option(capi.RT_OPT_ROW_FEEDBACK, fb)
+            best = None
+            for _ in range(2):
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                for c in cams:
+                    rend.render_device(c, depth, out.data_ptr(), prec, flags, capi.RT_OUT_RGB_F32,
+                                       row0=row0, nrows=nrows, stream=stream.cuda_stream)
+                e1.record(stream)
+                torch.cuda.synchronize(dev)
+                ms = e0.elapsed_time(e1) / len(cams)
+                best = ms if best is None else min(best, ms)
+            moving[f"ms_per_frame_row_feedback_{fb}"] = round(best, 4)
+        rend.set_option(capi.RT_OPT_ROW_FEEDBACK, args.row_feedback)
+
     result = None
     if rank == 0:
         ms_step = elapsed_s / args.steps * 1e3
@@ -330,6 +362,7 @@ def main() -> int:
             "cpu_baseline": None,
             "precision_sweep": sweep or None,
             "sun_extension": sun_ext,
+            "moving_camera": moving,
         }
         if world == 1 and not args.no_cpu_baseline and args.cpu_seconds > 0:
             result["cpu_baseline"] = cpu_baseline(cfg, prims, cam, depth, flags, args.cpu_seconds)

@@ -20,7 +20,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def counters(path):
     vals = {}
     for r in csv.DictReader(open(path)):
-        if "k_trace" not in r["Kernel_Name"]:
+        if "k_trace" not in r["Kernel_Name"] or "kst::" in r["Kernel_Name"]:  # sampled frames
             continue
         vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
     return {k: statistics.median(v) for k, v in vals.items()}
