@@ -62,7 +62,8 @@ struct rt_ctx {
     };
     Band cost_band;                // band of the pending snapshot
     Band fb_band;                  // band fb_perm was computed for
-    std::vector<int16_t> fb_perm;
+    std::vector<int16_t> fb_perm;  // over dispatch units: 2^fb_units_log2 per tile row
+    int fb_units_log2 = 0;
     int since_snapshot = 0;
     // the per-frame boxes depend only on the scene, the camera, the row band and the
     // options: a render with the same inputs as the previous one reuses them (the host
@@ -879,18 +880,32 @@ int rt_set_row_order(rt_ctx* ctx, const int16_t* perm, int32_t n) {
     return RT_OK;
 }
 
-/* Tile rows ordered by their most expensive wave (heaviest first; ties keep the lower
- * row), from a cost snapshot of gy rows x per_row waves. */
-static void order_rows(const uint16_t* cost, int gy, int per_row, std::vector<int16_t>& perm) {
-    std::vector<uint32_t> mx(gy, 0);
-    for (int r = 0; r < gy; r++) {
-        const uint16_t* c = cost + (size_t)r * per_row;
-        uint32_t m = 0;
-        for (int k = 0; k < per_row; k++) m = std::max<uint32_t>(m, c[k]);
-        mx[r] = m;
-    }
-    perm.resize(gy);
-    for (int r = 0; r < gy; r++) perm[r] = (int16_t)r;
+#ifndef RT_ROW_UNITS_MAX_LOG2
+#define RT_ROW_UNITS_MAX_LOG2 3
+#endif
+/* Dispatch units per tile row for the measured order (log2): rows split in up to 8 parts
+ * while the units fit row_perm and keep >= 8 tiles each — the ordering gets finer where a
+ * row holds both heavy and light tiles (replay of c2's measured wave times: whole rows
+ * -15%, quarter rows -19% vs centre-out). */
+static int units_log2(int gy, int gx) {
+    if (rt::BLOCK != 64) return 0;
+    for (int k = RT_ROW_UNITS_MAX_LOG2; k > 0; k--)
+        if ((gy << k) <= rt::ROW_PERM_MAX && ((gx + (1 << k) - 1) >> k) >= 8) return k;
+    return 0;
+}
+
+/* Dispatch units ordered by their most expensive wave (heaviest first; ties keep the lower
+ * unit), from a cost snapshot of gy rows x gx tiles (one wave per tile). */
+static void order_units(const uint16_t* cost, int gy, int gx, int ul, std::vector<int16_t>& perm) {
+    const int upr = 1 << ul, U = (gx + upr - 1) >> ul, nu = gy << ul;
+    std::vector<uint32_t> mx(nu, 0);
+    for (int r = 0; r < gy; r++)
+        for (int x = 0; x < gx; x++) {
+            uint32_t& m = mx[(r << ul) + x / U];
+            m = std::max<uint32_t>(m, cost[(size_t)r * gx + x]);
+        }
+    perm.resize(nu);
+    for (int u = 0; u < nu; u++) perm[u] = (int16_t)u;
     std::stable_sort(perm.begin(), perm.end(), [&](int16_t a, int16_t b) { return mx[a] > mx[b]; });
 }
 
@@ -904,16 +919,25 @@ static int prepare_rows(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t
     if (ctx->cost_pending && hipEventQuery(ctx->ev_cost) == hipSuccess) {
         ctx->cost_pending = false;
         const rt_ctx::Band& b = ctx->cost_band;
-        order_rows(ctx->h_cost, (b.nrows + rt::TILE_H - 1) / rt::TILE_H,
-                   ((b.W + rt::TILE_W - 1) / rt::TILE_W) * (rt::BLOCK / 64), ctx->fb_perm);
+        const int bgy = (b.nrows + rt::TILE_H - 1) / rt::TILE_H;
+        const int bgx = ((b.W + rt::TILE_W - 1) / rt::TILE_W) * (rt::BLOCK / 64);
+        ctx->fb_units_log2 = units_log2(bgy, bgx);
+        order_units(ctx->h_cost, bgy, bgx, ctx->fb_units_log2, ctx->fb_perm);
         ctx->fb_band = b;
     }
-    const std::vector<int16_t>* perm = nullptr;
-    if (!ctx->row_perm.empty()) perm = &ctx->row_perm;
-    else if (ctx->feedback > 0 && ctx->fb_band == band && !ctx->fb_perm.empty()) perm = &ctx->fb_perm;
-    if (perm && (int)perm->size() == gy && gy <= rt::ROW_PERM_MAX) {
-        p.row_perm_n = gy;
-        std::memcpy(p.row_perm, perm->data(), gy * sizeof(int16_t));
+    p.row_units_log2 = 0;
+    if (!ctx->row_perm.empty()) {
+        if ((int)ctx->row_perm.size() == gy && gy <= rt::ROW_PERM_MAX) {
+            p.row_perm_n = gy;
+            std::memcpy(p.row_perm, ctx->row_perm.data(), gy * sizeof(int16_t));
+        }
+    } else if (ctx->feedback > 0 && ctx->fb_band == band && !ctx->fb_perm.empty()) {
+        const int nu = gy << ctx->fb_units_log2;
+        if ((int)ctx->fb_perm.size() == nu && nu <= rt::ROW_PERM_MAX) {
+            p.row_units_log2 = ctx->fb_units_log2;
+            p.row_perm_n = nu;
+            std::memcpy(p.row_perm, ctx->fb_perm.data(), nu * sizeof(int16_t));
+        }
     }
     // sample this frame's costs when a snapshot is due (snapshot_costs copies them)
     p.tile_cost = nullptr;

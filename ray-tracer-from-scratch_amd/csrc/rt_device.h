@@ -145,7 +145,10 @@ struct KParams {
     int32_t row_center;         // tile row dispatched first (rt_trace.hip tile_row), -1 = off
     uint16_t* tile_cost;        // per wave (workgroup row-major over the frame's tiles, then
                                 // wave): shader cycles / 32, saturated; null = not recorded
-    int32_t row_perm_n;         // tile rows in row_perm (== the grid's rows), 0 = unused
+    int32_t row_units_log2;     // each tile row split into 2^k dispatch units (k > 0 only
+                                // with a row_perm over units: unit u = row (u >> k), part
+                                // (u & (2^k - 1)) of ceil(tiles / 2^k) tiles)
+    int32_t row_perm_n;         // dispatch units in row_perm (== the grid's rows), 0 = unused
     int16_t row_perm[ROW_PERM_MAX];  // dispatch order of tile rows (rt_trace.hip tile_row)
     PrimBox box[BIN_MAX_PRIMS]; // material-slot order: spheres, then walls
     int32_t mir_depth;          // wall-sequence levels with mirror boxes (0 = off)

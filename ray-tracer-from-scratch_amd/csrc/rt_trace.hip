@@ -1437,8 +1437,13 @@ template <int PREC, bool SUN, bool INT_EXP, bool CULL, int MAXD>
 __global__ void __launch_bounds__(BLOCK)
 __attribute__((amdgpu_waves_per_eu(waves_per_eu<PREC, SUN, INT_EXP, CULL, MAXD>(), 8)))
 k_trace(KParams p) {
-    trace_tile<PREC, SUN, INT_EXP, CULL, MAXD>(p, blockIdx.x, tile_row(p, blockIdx.y, gridDim.y),
-                                               gridDim.x);
+    // workgroup row -> dispatch unit (a tile row, or a part of one: KParams::row_units_log2)
+    const int u = tile_row(p, blockIdx.y, gridDim.y);
+    const int ul = p.row_units_log2;
+    const int bx = ((u & ((1 << ul) - 1)) * (int)gridDim.x) + (int)blockIdx.x;
+    const int gx = (p.W + TILE_W - 1) / TILE_W;
+    if (bx >= gx) return;  // the last part of a row may be short (wave-uniform)
+    trace_tile<PREC, SUN, INT_EXP, CULL, MAXD>(p, bx, u >> ul, gx);
 }
 
 template <int PREC, bool SUN, bool INT_EXP, bool CULL>
@@ -1489,7 +1494,9 @@ extern "C" int rt_diag_read(unsigned long long* out16) {
 
 int launch_trace_ns(const KParams& p, int prec, void* stream) {
     if (p.W <= 0 || p.nrows <= 0) return (int)hipSuccess;
-    const dim3 grid((p.W + TILE_W - 1) / TILE_W, (p.nrows + TILE_H - 1) / TILE_H);
+    const int ul = p.row_units_log2;
+    const dim3 grid((((p.W + TILE_W - 1) / TILE_W) + (1 << ul) - 1) >> ul,
+                    ((p.nrows + TILE_H - 1) / TILE_H) << ul);
     hipStream_t st = static_cast<hipStream_t>(stream);
     switch (prec) {
         case PREC_F64: return (int)launch_prec<PREC_F64>(p, grid, st);
