@@ -169,7 +169,7 @@ int rt_set_option(rt_ctx* ctx, int32_t option, int64_t value);
 /* Explicit dispatch order of the tile rows (8 pixel rows each): perm is a permutation of
  * 0..n-1, used by every render whose band has exactly n tile rows, ahead of
  * RT_OPT_ROW_FEEDBACK; n = 0 clears it.  Scheduling only: output is identical.
- * RT_ERR_INVALID_ARG if perm is not a permutation or n > 1024. */
+ * RT_ERR_INVALID_ARG if perm is not a permutation or n > 2048. */
 int rt_set_row_order(rt_ctx* ctx, const int16_t* perm, int32_t n);
 
 /* ---- frame operators (replace rt_scene, main.cpp:124-139) --------------- */

@@ -113,10 +113,10 @@ struct PrimBox {
     int16_t x0, x1, i0, i1;  // inclusive pixel box (frame rows); x0 > x1 = never hit
 };
 
-// Tile-row dispatch order given explicitly (up to ROW_PERM_MAX tile rows, 8-row tiles:
-// 8192 pixel rows).
+// Dispatch order given explicitly: up to ROW_PERM_MAX units (tile rows of 8 pixel rows, or
+// parts of them), int16 each, in the kernel arguments.
 #ifndef RT_ROW_PERM_MAX
-#define RT_ROW_PERM_MAX 1024
+#define RT_ROW_PERM_MAX 2048
 #endif
 constexpr int ROW_PERM_MAX = RT_ROW_PERM_MAX;
 
@@ -160,6 +160,9 @@ struct KParams {
     double eye_s[EYE_MAX_S][4];         // sphere s: {oc.x, oc.y, oc.z, |oc|^2 - r^2}
     double eye_w[EYE_MAX_W];            // wall w: dot(P - pos, n)
 };
+// by-value kernel arguments of up to 16 KB arrive intact (tools/ubench/kernarg_size.hip,
+// kernarg_stale.hip: consistent across back-to-back launches)
+static_assert(sizeof(KParams) <= 16384, "kernel arguments over 16 KB");
 
 // Host-side launchers (rt_trace.hip).  Return a hipError_t as int.
 int launch_trace(const KParams& p, int prec, void* stream);
