@@ -102,6 +102,9 @@ def main() -> int:
     ap.add_argument("--config", default="c2", choices=sorted(scenes.CONFIGS))
     ap.add_argument("--precision", default="path64", choices=sorted(capi.PRECISIONS))
     ap.add_argument("--mode", default="frames", choices=["frames", "tiled"])
+    ap.add_argument("--out", default="rgb_f32", choices=["rgb_f32", "rgba8"],
+                    help="timed output format: linear fp32 RGB (12 B/px, parity buffer) or the "
+                         "clamp+truncate RGBA8 epilogue (4 B/px; cuts the tiled gather 3x)")
     ap.add_argument("--sun", action="store_true", help="build-defined sun term (off = parity)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -160,19 +163,23 @@ def main() -> int:
     # default stream (handle 0) would put the launches and the timing events apart
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
+    # sized for fp32 RGB: the per-precision sweep below always writes 12 B/px into it
     out = torch.empty((band_max, W, 3), dtype=torch.float32, device=dev)
+    out_fmt = capi.RT_OUT_RGBA8 if args.out == "rgba8" else capi.RT_OUT_RGB_F32
     segs_t = torch.zeros(1, dtype=torch.int64, device=dev)
 
     def launch(d_segs: int = 0, dst=None):
         rend.render_device(cam, depth, (dst if dst is not None else out).data_ptr(), prec, flags,
-                           capi.RT_OUT_RGB_F32, row0=row0, nrows=nrows, d_segments=d_segs,
+                           out_fmt, row0=row0, nrows=nrows, d_segments=d_segs,
                            stream=stream.cuda_stream)
 
     tiled = None
     if args.mode == "tiled" and world > 1:
         from rtamd import tiling
         # double-buffered: the gather of frame k (RCCL stream) overlaps the render of k+1
-        tiled = tiling.TiledFrames(lambda r0, n, buf: launch(dst=buf), H, W, 3, torch.float32,
+        tiled = tiling.TiledFrames(lambda r0, n, buf: launch(dst=buf), H, W,
+                                   4 if args.out == "rgba8" else 3,
+                                   torch.uint8 if args.out == "rgba8" else torch.float32,
                                    dev, depth=2)
 
     def step():
@@ -302,10 +309,12 @@ def main() -> int:
         frames_per_step = world if args.mode == "frames" else 1
         px_step = W * H * frames_per_step
         kernel_s = kernel_ms * 1e-3
-        out_bytes = nrows * W * 12
+        out_bytes = nrows * W * (4 if args.out == "rgba8" else 12)
         alg_bytes = out_bytes + scene_bytes(n_sph, n_wall, len(sc))
         workload = f"{cfg.name}:{W}x{H}:d{depth}:s{n_sph}w{n_wall}"
-        traffic = load_traffic(args.traffic_json, workload, args.precision)
+        # PMC traffic was collected on the fp32 RGB output only
+        traffic = (load_traffic(args.traffic_json, workload, args.precision)
+                   if args.out == "rgb_f32" else None)
         flops = my_segs * flop_per_segment(n_sph, n_wall)
         valu_peak = VALU_PEAK_TFLOPS[args.precision]
         result = {
@@ -327,6 +336,7 @@ def main() -> int:
                 "width": W, "height": H, "depth": depth,
                 "spheres": n_sph, "walls": n_wall,
                 "precision": args.precision,
+                "output": args.out,
                 "parity": PARITY[args.precision],
                 "frames_per_step": frames_per_step,
                 "segments_per_step": total_segs,

@@ -11,7 +11,7 @@ ROUND=${ROUND:-r01}; OUT=gpurun_out/prof_$ROUND
 CONFIGS=${CONFIGS:-c2}; PRECS=${PRECS:-path64 f64 f32}
 mkdir -p "$OUT"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/bench" -o bench -- \
-    python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-sweep > "$OUT/bench.json" 2> "$OUT/bench.err" \
+    python3 bench.py --steps 200 --warmup 40 --no-cpu-baseline --no-sweep > "$OUT/bench.json" 2> "$OUT/bench.err" \
     || { echo "bench trace failed"; exit 1; }
 echo "bench trace ok"
 for cfg in $CONFIGS; do
