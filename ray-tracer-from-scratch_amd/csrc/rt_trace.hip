@@ -792,7 +792,14 @@ __device__ __forceinline__ f3 tof(d3 v) { return F3((float)v.x, (float)v.y, (flo
  * light one: the dispatcher goes row by row, so rows are visited centre-out from the
  * host's estimate of the heaviest row (KParams::row_center, rt_capi.cpp) — heavy work
  * first, the cheap rows fill in around it.  Identity when row_center < 0. */
+#ifndef RT_PERM_FIRST      // A/B knob: 1 = take the explicit order when it covers the grid
+#define RT_PERM_FIRST 0    // (wave-uniform branch) and skip the centre-out arithmetic
+#endif
 __device__ __forceinline__ int tile_row(const KParams& p, int j, int n) {
+    if (RT_PERM_FIRST && p.row_perm_n == n) {
+        const uint32_t w = reinterpret_cast<const uint32_t*>(p.row_perm)[min(j >> 1, ROW_PERM_MAX / 2 - 1)];
+        return (int16_t)((j & 1) ? (w >> 16) : (w & 0xffff));
+    }
     // branch-free (scalar selects), so that its kernel-argument loads — including the dword
     // holding entry j of an explicit order (a 16-bit load would be a vector load) — issue in
     // the wave's first batch instead of one dependent round trip after another

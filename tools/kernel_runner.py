@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--precision", default="mixed")
     ap.add_argument("--launches", type=int, default=10)
     ap.add_argument("--sun", action="store_true")
+    ap.add_argument("--depth", type=int, default=-1, help="-1 = the config's depth")
     args = ap.parse_args()
     import torch
     dev = torch.device("cuda", 0)
@@ -28,7 +29,7 @@ def main():
     cam = capi.camera_init(**scenes.camera_args(cfg.width, cfg.height))
     out = torch.empty((cam.height, cam.width, 3), dtype=torch.float32, device=dev)
     for _ in range(args.launches):
-        rend.render_device(cam, cfg.depth, out.data_ptr(), capi.PRECISIONS[args.precision],
+        rend.render_device(cam, cfg.depth if args.depth < 0 else args.depth, out.data_ptr(), capi.PRECISIONS[args.precision],
                            capi.RT_FLAG_SUN if args.sun else 0, capi.RT_OUT_RGB_F32,
                            stream=stream.cuda_stream)
     torch.cuda.synchronize()
