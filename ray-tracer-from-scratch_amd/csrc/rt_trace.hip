@@ -792,19 +792,22 @@ __device__ __forceinline__ f3 tof(d3 v) { return F3((float)v.x, (float)v.y, (flo
  * light one: the dispatcher goes row by row, so rows are visited centre-out from the
  * host's estimate of the heaviest row (KParams::row_center, rt_capi.cpp) — heavy work
  * first, the cheap rows fill in around it.  Identity when row_center < 0. */
+// Wave-start loads.  1: no early return before the trace (a workgroup past the end of a
+// row part runs with every lane invalid) and the primary box load is unconditional, so it
+// no longer waits on nbox (A/B: c2 PATH64 -0.1..1.3%, F32 -1.3..2.6%, c1 -1..4.5%, c3
+// +-0.6%).  2: also every wave-start kernel-argument value in ONE batch with one wait,
+// pinned by an empty asm (A/B: c2 PATH64 +15%, F64 +7% — slower, off).
+#ifndef RT_EARLY_LOADS
+#define RT_EARLY_LOADS 1
+#endif
 #ifndef RT_PERM_FIRST      // A/B knob: 1 = take the explicit order when it covers the grid
 #define RT_PERM_FIRST 0    // (wave-uniform branch) and skip the centre-out arithmetic
 #endif
-__device__ __forceinline__ int tile_row(const KParams& p, int j, int n) {
-    if (RT_PERM_FIRST && p.row_perm_n == n) {
-        const uint32_t w = reinterpret_cast<const uint32_t*>(p.row_perm)[min(j >> 1, ROW_PERM_MAX / 2 - 1)];
-        return (int16_t)((j & 1) ? (w >> 16) : (w & 0xffff));
-    }
-    // branch-free (scalar selects), so that its kernel-argument loads — including the dword
-    // holding entry j of an explicit order (a 16-bit load would be a vector load) — issue in
-    // the wave's first batch instead of one dependent round trip after another
-    const int c = p.row_center, rpn = p.row_perm_n;
-    const uint32_t w = reinterpret_cast<const uint32_t*>(p.row_perm)[min(j >> 1, ROW_PERM_MAX / 2 - 1)];
+__device__ __forceinline__ uint32_t row_perm_word(const KParams& p, int j) {
+    return reinterpret_cast<const uint32_t*>(p.row_perm)[min(j >> 1, ROW_PERM_MAX / 2 - 1)];
+}
+/* c = row_center, rpn = row_perm_n, w = row_perm_word(j): the loaded values */
+__device__ __forceinline__ int tile_row_of(int c, int rpn, uint32_t w, int j, int n) {
     const int L = min(c, n - 1 - c);  // rows c-L .. c+L alternate
     const int d = (j + 1) >> 1;
     const int alt = (j & 1) ? c + d : c - d;
@@ -814,6 +817,16 @@ __device__ __forceinline__ int tile_row(const KParams& p, int j, int n) {
     t = (c < 0 || c >= n) ? j : t;
     const int pj = (int16_t)((j & 1) ? (w >> 16) : (w & 0xffff));
     return rpn == n ? pj : t;
+}
+__device__ __forceinline__ int tile_row(const KParams& p, int j, int n) {
+    if (RT_PERM_FIRST && p.row_perm_n == n) {
+        const uint32_t w = row_perm_word(p, j);
+        return (int16_t)((j & 1) ? (w >> 16) : (w & 0xffff));
+    }
+    // branch-free (scalar selects), so that its kernel-argument loads — including the dword
+    // holding entry j of an explicit order (a 16-bit load would be a vector load) — issue in
+    // the wave's first batch instead of one dependent round trip after another
+    return tile_row_of(p.row_center, p.row_perm_n, row_perm_word(p, j), j, n);
 }
 
 __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
@@ -840,6 +853,14 @@ __device__ __forceinline__ TileO tile_origin(int x, int i) {
     const int lane = threadIdx.x & 63;
     return {__builtin_amdgcn_readfirstlane(x - (lane & 7)),
             __builtin_amdgcn_readfirstlane(i - (lane >> 3))};
+}
+/* The primary boxes: p.box always holds BIN_MAX_PRIMS (= 64) entries, so lane l's load is
+ * in bounds whatever nbox is; the select after it needs nbox, the load does not. */
+__device__ __forceinline__ uint64_t box_load_primary(const KParams& p) {
+    static_assert(BIN_MAX_PRIMS == 64, "one box per lane");
+    const int l = threadIdx.x & 63;
+    const uint64_t v = *reinterpret_cast<const uint64_t*>(p.box + l);
+    return l < p.nbox ? v : 0x80007fff80007fffull;
 }
 __device__ __forceinline__ uint64_t box_keep(uint64_t raw, TileO t) {
     const int x0 = (int16_t)(raw & 0xffff), x1 = (int16_t)((raw >> 16) & 0xffff);
@@ -944,11 +965,12 @@ __device__ __forceinline__ HitD scan_d(const KParams& p, const RayD& r, bool ali
  * MIXED, the parity modes); otherwise in fp32 (PATH64). */
 template <bool MIXED, bool COLOR64, bool SUN, bool INT_EXP, bool CULL, int MAXD>
 __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool alive,
-                                            int& segs, uint64_t& t_start) {
+                                            int& segs, uint64_t& t_start, uint64_t braw_in) {
     using CT = typename std::conditional<COLOR64, double, float>::type;
     const d3 cpos = ld3(p.pos);
     const d3 pc = (ld3(p.tl) + ld3(p.dx) * (double)x) + ld3(p.dy) * (double)i;  // main.cpp:132
-    const uint64_t braw = CULL ? 0 : box_load(p, p.box);  // branch-free: issued first
+    const uint64_t braw = CULL ? 0 : (RT_EARLY_LOADS >= 2 ? braw_in
+                                   : RT_EARLY_LOADS ? box_load_primary(p) : box_load(p, p.box));
     // main.cpp:133-134 (direction not normalised); the sphere terms only where needed
     // (PATH64: the fp32 terminal segment needs none of them)
     constexpr bool LAZY = RT_LAZY_TERMS && !COLOR64 && !CULL && RT_TERMINAL_F32;
@@ -1196,7 +1218,7 @@ __device__ __forceinline__ void walls_f(const KParams& p, f3 o, f3 d, float& bes
 
 template <bool SUN, bool CULL, int MAXD>
 __device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, bool alive,
-                                            int& segs, uint64_t& t_start) {
+                                            int& segs, uint64_t& t_start, uint64_t braw_in) {
     const d3 pcd = (ld3(p.tl) + ld3(p.dx) * (double)x) + ld3(p.dy) * (double)i;
     const d3 dd = ld3(p.pos) - pcd;
     f3 o = F3((float)p.pos[0], (float)p.pos[1], (float)p.pos[2]);
@@ -1210,7 +1232,13 @@ __device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, bool
     f3 c = F3(0.f, 0.f, 0.f);
     t_start = RT_STAMP ? __builtin_amdgcn_s_memtime() : 0;  // see trace_pixel_d
     const TileO tile = tile_origin(x, i);
+#if RT_EARLY_LOADS >= 2
+    // unconditional compare (all lanes active), so the wave-start box load is not sunk
+    uint64_t keep = CULL ? ~0ull : box_keep(braw_in, tile);
+    if (p.nbox <= 0) keep = ~0ull;
+#else
     const uint64_t keep = (!CULL && p.nbox > 0) ? tile_keep(p, p.box, tile) : ~0ull;
+#endif
     int kend = 0;  // wave-uniform: bounce iterations run (every lane's n <= kend)
     for (int k = 0;; ++k) {
         if (!__any(alive)) {
@@ -1399,7 +1427,8 @@ constexpr int waves_per_eu() {
 
 /* One tile per wave: tile column bx, tile row trow (after the row order), gx tile columns. */
 template <int PREC, bool SUN, bool INT_EXP, bool CULL, int MAXD>
-__device__ __forceinline__ void trace_tile(const KParams& p, int bx, int trow, int gx) {
+__device__ __forceinline__ void trace_tile(const KParams& p, int bx, int trow, int gx,
+                                           uint64_t braw) {
 #if RT_WAVE_TIMES
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -1413,16 +1442,16 @@ __device__ __forceinline__ void trace_tile(const KParams& p, int bx, int trow, i
     int segs = 0;
     // every lane runs the (converged) bounce loop; only valid lanes trace and store
     if (PREC == PREC_F32) {
-        const f3 c = trace_pixel_f<SUN, CULL, MAXD>(p, x, i, valid, segs, t_tile);
+        const f3 c = trace_pixel_f<SUN, CULL, MAXD>(p, x, i, valid, segs, t_tile, braw);
         if (valid) store_pixel(p, r, x, c.x, c.y, c.z);
     } else {
         const d3 c =
             trace_pixel_d<PREC == PREC_MIXED, PREC != PREC_PATH64, SUN, INT_EXP, CULL, MAXD>(
-                p, x, i, valid, segs, t_tile);
+                p, x, i, valid, segs, t_tile, braw);
         if (valid) store_pixel(p, r, x, c.x, c.y, c.z);
     }
     count_segments(p, segs);
-    if (RT_STAMP && lane == 0) {
+    if (RT_STAMP && lane == 0 && bx < gx) {
         // this tile's cost for the host's next tile-row order (rt_capi.cpp row feedback)
         const uint64_t c = (__builtin_amdgcn_s_memtime() - t_tile) >> 5;
         p.tile_cost[((size_t)trow * gx + bx) * (BLOCK / 64) + wave] = (uint16_t)(c < 65535 ? c : 65535);
@@ -1430,7 +1459,7 @@ __device__ __forceinline__ void trace_tile(const KParams& p, int bx, int trow, i
 #if RT_WAVE_TIMES
     // diagnostic build: per wave {start, end, segments << 32 | CU id} (100 MHz clock)
     for (int off = 32; off > 0; off >>= 1) segs += __shfl_xor(segs, off, 64);
-    if (p.stats != nullptr && lane == 0) {
+    if (p.stats != nullptr && lane == 0 && bx < gx) {
         const size_t wid = ((size_t)trow * gx + bx) * (BLOCK / 64) + wave;
         p.stats[3 * wid] = t_start;
         p.stats[3 * wid + 1] = __builtin_amdgcn_s_memrealtime();
@@ -1445,12 +1474,34 @@ __global__ void __launch_bounds__(BLOCK)
 __attribute__((amdgpu_waves_per_eu(waves_per_eu<PREC, SUN, INT_EXP, CULL, MAXD>(), 8)))
 k_trace(KParams p) {
     // workgroup row -> dispatch unit (a tile row, or a part of one: KParams::row_units_log2)
+    // the primary pixel boxes (one per lane; wave-start load, used after ray generation)
+    const uint64_t braw = (RT_EARLY_LOADS >= 2 && !CULL) ? box_load_primary(p) : 0;
+#if RT_EARLY_LOADS >= 2
+    // every kernel-argument value the wave start needs — the dispatch order's entry and ray
+    // generation's scalars (main.cpp:132) — loaded in one batch with one wait
+    const int j = blockIdx.y;
+    const uint32_t pw = row_perm_word(p, j);
+    const int rc = p.row_center, rpn = p.row_perm_n;
+    {
+        const double a0 = p.pos[0], a1 = p.pos[1], a2 = p.pos[2], b0 = p.tl[0], b1 = p.tl[1],
+                     b2 = p.tl[2], c0 = p.dx[0], c1 = p.dx[1], c2 = p.dx[2], e0 = p.dy[0],
+                     e1 = p.dy[1], e2 = p.dy[2];
+        asm volatile("" ::"s"(a0), "s"(a1), "s"(a2), "s"(b0), "s"(b1), "s"(b2), "s"(c0),
+                     "s"(c1), "s"(c2), "s"(e0), "s"(e1), "s"(e2), "s"(p.W), "s"(p.row0),
+                     "s"(p.nbox), "s"(pw), "s"(rc), "s"(rpn), "s"(p.row_units_log2),
+                     "s"(gridDim.x), "s"(gridDim.y));
+    }
+    const int u = tile_row_of(rc, rpn, pw, j, gridDim.y);
+#else
     const int u = tile_row(p, blockIdx.y, gridDim.y);
+#endif
     const int ul = p.row_units_log2;
     const int bx = ((u & ((1 << ul) - 1)) * (int)gridDim.x) + (int)blockIdx.x;
     const int gx = (p.W + TILE_W - 1) / TILE_W;
-    if (bx >= gx) return;  // the last part of a row may be short (wave-uniform)
-    trace_tile<PREC, SUN, INT_EXP, CULL, MAXD>(p, bx, u >> ul, gx);
+    // the last part of a row may be short (wave-uniform): such a wave's lanes are all
+    // invalid (x >= W), so it can also run through with nothing to trace or store
+    if (!RT_EARLY_LOADS && bx >= gx) return;
+    trace_tile<PREC, SUN, INT_EXP, CULL, MAXD>(p, bx, u >> ul, gx, braw);
 }
 
 template <int PREC, bool SUN, bool INT_EXP, bool CULL>
