@@ -160,7 +160,27 @@ __device__ __forceinline__ double div_r(double a, double b, double r) {
 /* sqrt(x) correctly rounded: LLVM's fp64 sqrt sequence (rsq + Goldschmidt/Newton
  * refinement) without its range scaling, which is the identity for x >= 2^-767; smaller
  * (and zero/negative) arguments take the library path. */
+#ifndef RT_SQRT_UNIFORM   // 1: the rare-argument fallback behind a wave-uniform test (one
+#define RT_SQRT_UNIFORM 0 // ballot) instead of a divergent branch (exec-mask save/restore)
+#endif
+__device__ __forceinline__ double sqrt_fast(double x) {
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y;
+    double h = y * 0.5;
+    const double r = __builtin_fma(-h, g, 0.5);
+    g = __builtin_fma(g, r, g);
+    double d = __builtin_fma(-g, g, x);
+    h = __builtin_fma(h, r, h);
+    g = __builtin_fma(d, h, g);
+    d = __builtin_fma(-g, g, x);
+    return __builtin_fma(d, h, g);
+}
 __device__ __forceinline__ double sqrt_e(double x) {
+    if (RT_SQRT_UNIFORM) {
+        const bool ok = x >= 0x1p-767;
+        if (__builtin_expect(__ballot(!ok) != 0, 0)) return ok ? sqrt_fast(x) : sqrt(x);
+        return sqrt_fast(x);
+    }
     if (!(x >= 0x1p-767)) return sqrt(x);
     const double y = __builtin_amdgcn_rsq(x);
     double g = x * y;
