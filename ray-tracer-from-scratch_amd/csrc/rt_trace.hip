@@ -820,6 +820,9 @@ __device__ __forceinline__ f3 tof(d3 v) { return F3((float)v.x, (float)v.y, (flo
 #ifndef RT_EARLY_LOADS
 #define RT_EARLY_LOADS 1
 #endif
+#ifndef RT_TILE_PAIRS      // 1: each wave traces two tiles one after the other — dispatch
+#define RT_TILE_PAIRS 0    // unit j and unit n-1-j of the row order (heavy with light), so
+#endif                     // the per-wave start cost is paid once per 128 pixels (A/B knob)
 #ifndef RT_PERM_FIRST      // A/B knob: 1 = take the explicit order when it covers the grid
 #define RT_PERM_FIRST 0    // (wave-uniform branch) and skip the centre-out arithmetic
 #endif
@@ -1496,6 +1499,11 @@ k_trace(KParams p) {
     // workgroup row -> dispatch unit (a tile row, or a part of one: KParams::row_units_log2)
     // the primary pixel boxes (one per lane; wave-start load, used after ray generation)
     const uint64_t braw = (RT_EARLY_LOADS >= 2 && !CULL) ? box_load_primary(p) : 0;
+    // dispatch units of the row order (tile rows or parts of them); with tile pairs the grid
+    // has half as many rows
+    const int n_units = RT_TILE_PAIRS
+                            ? (((p.nrows + TILE_H - 1) / TILE_H) << p.row_units_log2)
+                            : (int)gridDim.y;
 #if RT_EARLY_LOADS >= 2
     // every kernel-argument value the wave start needs — the dispatch order's entry and ray
     // generation's scalars (main.cpp:132) — loaded in one batch with one wait
@@ -1511,17 +1519,29 @@ k_trace(KParams p) {
                      "s"(p.nbox), "s"(pw), "s"(rc), "s"(rpn), "s"(p.row_units_log2),
                      "s"(gridDim.x), "s"(gridDim.y));
     }
-    const int u = tile_row_of(rc, rpn, pw, j, gridDim.y);
+    const int u = tile_row_of(rc, rpn, pw, j, n_units);
 #else
-    const int u = tile_row(p, blockIdx.y, gridDim.y);
+    const int u = tile_row(p, blockIdx.y, n_units);
 #endif
     const int ul = p.row_units_log2;
-    const int bx = ((u & ((1 << ul) - 1)) * (int)gridDim.x) + (int)blockIdx.x;
     const int gx = (p.W + TILE_W - 1) / TILE_W;
+#if RT_TILE_PAIRS
+    // grid.y = ceil(units / 2): unit j, then unit n-1-j (none when they coincide)
+    const int j1 = n_units - 1 - (int)blockIdx.y;
+    const int u1 = tile_row(p, j1, n_units);
+    const int bx0 = ((u & ((1 << ul) - 1)) * (int)gridDim.x) + (int)blockIdx.x;
+    const int bx1 = ((u1 & ((1 << ul) - 1)) * (int)gridDim.x) + (int)blockIdx.x;
+    trace_tile<PREC, SUN, INT_EXP, CULL, MAXD>(p, bx0, u >> ul, gx, braw);
+    if (j1 > (int)blockIdx.y)
+        trace_tile<PREC, SUN, INT_EXP, CULL, MAXD>(p, bx1, u1 >> ul, gx,
+                                                   (RT_EARLY_LOADS >= 2 && !CULL) ? box_load_primary(p) : 0);
+#else
+    const int bx = ((u & ((1 << ul) - 1)) * (int)gridDim.x) + (int)blockIdx.x;
     // the last part of a row may be short (wave-uniform): such a wave's lanes are all
     // invalid (x >= W), so it can also run through with nothing to trace or store
     if (!RT_EARLY_LOADS && bx >= gx) return;
     trace_tile<PREC, SUN, INT_EXP, CULL, MAXD>(p, bx, u >> ul, gx, braw);
+#endif
 }
 
 template <int PREC, bool SUN, bool INT_EXP, bool CULL>
@@ -1573,8 +1593,9 @@ extern "C" int rt_diag_read(unsigned long long* out16) {
 int launch_trace_ns(const KParams& p, int prec, void* stream) {
     if (p.W <= 0 || p.nrows <= 0) return (int)hipSuccess;
     const int ul = p.row_units_log2;
+    const int units = ((p.nrows + TILE_H - 1) / TILE_H) << ul;
     const dim3 grid((((p.W + TILE_W - 1) / TILE_W) + (1 << ul) - 1) >> ul,
-                    ((p.nrows + TILE_H - 1) / TILE_H) << ul);
+                    RT_TILE_PAIRS ? (units + 1) / 2 : units);
     hipStream_t st = static_cast<hipStream_t>(stream);
     switch (prec) {
         case PREC_F64: return (int)launch_prec<PREC_F64>(p, grid, st);
