@@ -106,6 +106,9 @@ __device__ unsigned long long g_diag[16];
 #ifndef RT_WPE_MIXED_CULL_DROP  // MIXED cull kernels at depth > 4: one wave less
 #define RT_WPE_MIXED_CULL_DROP 1
 #endif
+#ifndef RT_WPE_F32_BONUS
+#define RT_WPE_F32_BONUS 0
+#endif
 #ifndef RT_WPE_F64_LIN_BONUS
 #define RT_WPE_F64_LIN_BONUS 0
 #endif
@@ -1438,7 +1441,7 @@ constexpr int waves_per_eu() {
     int w = 0;
     if (PREC == PREC_F64 && !CULL && !SUN && tier == 0) return 4 + RT_WPE_F64_LIN_BONUS;
     if (PREC == PREC_F32)
-        w = 5 - (tier > 0 ? 1 : 0) - ((SUN && tier == 2) ? 1 : 0);
+        w = 5 + RT_WPE_F32_BONUS - (tier > 0 ? 1 : 0) - ((SUN && tier == 2) ? 1 : 0);
     else if (PREC == PREC_PATH64)
         w = RT_WPE_PATH64 - (tier == 2 ? 1 : 0) - ((SUN && tier > 0) ? 1 : 0) +
             ((!CULL && !SUN && tier == 0) ? RT_WPE_PATH64_LIN_BONUS : 0);

@@ -10,9 +10,11 @@ sys.path.insert(0, os.path.join(REPO, "ray-tracer-from-scratch_amd"))
 from rtamd import capi, scenes  # noqa: E402
 
 
-def main():
+def main():  # depth_probe.py [config] [precision] [lib]
     import torch
     dev = torch.device("cuda", 0)
+    if len(sys.argv) > 3:  # an A/B build of librt_amd.so
+        capi._lib = capi.load(sys.argv[3])
     cfg = scenes.CONFIGS[sys.argv[1] if len(sys.argv) > 1 else "c2"]
     prec = capi.PRECISIONS[sys.argv[2] if len(sys.argv) > 2 else "path64"]
     cam = capi.camera_init(**scenes.camera_args(cfg.width, cfg.height))
