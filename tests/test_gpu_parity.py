@@ -457,7 +457,10 @@ def test_row_order_is_output_invariant(rend):
     sc = scenes.synthetic_scene(8, 4)
     rend.set_scene(scenes.to_prims(sc))
     try:
-        for w, h, r0, n in ((160, 90, 0, 90), (203, 117, 13, 71), (64, 36, 35, 1)):
+        # (200, 64): 25 tile columns in 2 dispatch parts of 13, so one workgroup of each
+        # tile row lies past the row's end (every lane invalid, no store, no cost stamp)
+        for w, h, r0, n in ((160, 90, 0, 90), (203, 117, 13, 71), (64, 36, 35, 1),
+                            (200, 64, 0, 64)):
             cam = capi.camera_init(**scenes.camera_args(w, h))
             imgs = []
             for on in (1, 0):
