@@ -100,10 +100,23 @@ enum rt_precision {
                             arithmetic: no discontinuity flips, colours within ~1e-6 */
 };
 
+/* The reference's only post-step is SDL_MapRGB(format, val.x*255, ...) (main.cpp:345),
+ * whose Uint8 parameters take the double by implicit conversion.  For 0 <= v*255 < 256
+ * that truncates toward zero; above (local colour can reach color*1.4: diffuse .9 +
+ * specular .4 + ambient .1) the conversion is undefined in C++, and the reference's
+ * x86-64 build (g++ -O3: cvttsd2si, then the low byte) WRAPS modulo 256 — a highlight of
+ * 1.084 displays as 20.  RT_OUT_RGBA8 deliberately deviates there and saturates at 255
+ * (the tone-map epilogue); RT_OUT_RGBA8_WRAP reproduces the x86-64 bytes exactly
+ * (tests/golden/surface.npz, recorded from that conversion compiled by g++). */
 enum rt_out_format {
     RT_OUT_RGB_F32 = 0,  /* H x W x 3 float, row-major, linear unclamped RGB (12 B/px) */
     RT_OUT_RGB_F64 = 1,  /* H x W x 3 double (24 B/px) — exact drop-in for vector<vector<RGB>> */
-    RT_OUT_RGBA8 = 2     /* H x W x 4 uint8 (R,G,B,255): clamp(v,0,1)*255 truncated (main.cpp:345) */
+    RT_OUT_RGBA8 = 2,    /* H x W x 4 uint8 (R,G,B,255): trunc(clamp(v,0,1)*255).  Equals
+                            main.cpp:345 for in-range pixels; saturates (a deliberate
+                            deviation) where the reference's conversion wraps */
+    RT_OUT_RGBA8_WRAP = 3 /* H x W x 4 uint8 (R,G,B,255): (uint8)(int32)trunc(v*255), i.e.
+                            main.cpp:345's bytes on x86-64 for every value, out-of-range
+                            (wraps mod 256) and NaN (0) included */
 };
 
 enum rt_flags {

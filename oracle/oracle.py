@@ -59,6 +59,7 @@ class Oracle:
                                         _P(C.c_uint64), C.c_int]),
             "orc_synthetic_scene": (C.c_int, [C.c_int, C.c_int, C.c_uint64, _prim_p, _dp]),
             "orc_default_scene": (C.c_int, [_prim_p, _dp]),
+            "orc_surface_u8": (None, [_dp, C.c_size_t, _P(C.c_uint8)]),
         }
         for name, (res, args) in sig.items():
             f = getattr(lib, name)
@@ -135,6 +136,14 @@ class Oracle:
                                             C.byref(dist), n)
         return idx, dist.value, tuple(n)
 
+    def surface_u8(self, rgb):
+        """main.cpp:345's bytes (x86-64 conversion restated): [..., 3] float64 -> uint8."""
+        a = np.ascontiguousarray(rgb, np.float64)
+        out = np.empty(a.shape, np.uint8)
+        self.lib.orc_surface_u8(a.ctypes.data_as(_dp), a.size // 3,
+                                out.ctypes.data_as(_P(C.c_uint8)))
+        return out
+
     def synthetic_scene(self, n_spheres, n_walls, seed=1234):
         arr = (capi.rt_prim * max(1, n_spheres + n_walls))()
         raw = (C.c_double * max(3, 3 * n_walls))()
@@ -165,6 +174,7 @@ class Reference:
             "ref_specular": (C.c_double, [_dp, _dp, _dp, _dp]),
             "ref_reflect": (None, [_dp, _dp, _dp]),
             "ref_normalize": (None, [_dp, _dp]),
+            "ref_surface_u8": (None, [_dp, C.c_size_t, _P(C.c_uint8)]),
         }
         for name, (res, args) in sig.items():
             f = getattr(lib, name)
@@ -181,6 +191,14 @@ class Reference:
         h = self.lib.ref_camera_init(_arr(position), _arr(lookat), _arr(vup), vfov, aspect_ratio,
                                      image_width, out)
         return h, np.array(list(out)).reshape(4, 3)
+
+    def surface_u8(self, rgb):
+        """main.cpp:345's conversion as the reference's g++ -O3 build performs it."""
+        a = np.ascontiguousarray(rgb, np.float64)
+        out = np.empty(a.shape, np.uint8)
+        self.lib.ref_surface_u8(a.ctypes.data_as(_dp), a.size // 3,
+                                out.ctypes.data_as(_P(C.c_uint8)))
+        return out
 
     def render(self, prims, raw, cam_args, depth):
         W = int(cam_args["image_width"])

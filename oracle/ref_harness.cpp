@@ -160,6 +160,23 @@ void ref_wall_intersect(const double* position, const double* raw_normal, double
     *dist = c.distance; S(normal, c.normal); *hit = c.hit;
 }
 
+/* main.cpp:345's surface packing: SDL_MapRGB(format, val.x * 255, val.y * 255, val.z * 255)
+ * takes Uint8 parameters, so each double converts implicitly at the call — undefined above
+ * 255 in C++; what this g++ -O3 x86-64 build does (the reference's CMake flags) is recorded
+ * as fixtures.  pack_rgb has SDL_MapRGB's parameter types; the call has main.cpp's form. */
+typedef uint8_t Uint8;
+static __attribute__((noinline)) void pack_rgb(Uint8* out, Uint8 r, Uint8 g, Uint8 b) {
+    out[0] = r;
+    out[1] = g;
+    out[2] = b;
+}
+void ref_surface_u8(const double* rgb, size_t npx, uint8_t* out) {
+    for (size_t k = 0; k < npx; k++) {
+        const RGB val(rgb[3 * k], rgb[3 * k + 1], rgb[3 * k + 2]);
+        pack_rgb(out + 3 * k, val.x * 255, val.y * 255, val.z * 255);
+    }
+}
+
 void ref_out_color(const double* v, double rgb[3]) { S(rgb, out_color(V(v))); }
 double ref_diffuse_shading(const double* pos, const double* normal, const double* light) {
     return diffuse_shading(V(pos), V(normal), V(light));

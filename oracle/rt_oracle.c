@@ -362,3 +362,16 @@ int orc_synthetic_scene(int n_spheres, int n_walls, uint64_t seed, rt_prim* out,
     }
     return k;
 }
+
+/* main.cpp:345: SDL_MapRGB(surface->format, val.x * 255, val.y * 255, val.z * 255) with
+ * Uint8 parameters.  The reference's x86-64 build converts with cvttsd2si (truncation to
+ * int32; NaN and values outside the int32 range give INT32_MIN) and keeps the low byte:
+ * in-range pixels truncate, highlights above 1.0 wrap modulo 256. */
+static uint8_t surface_byte(double v) {
+    const double t = v * 255;
+    const int32_t i = (t > -2147483649.0 && t < 2147483648.0) ? (int32_t)t : INT32_MIN;
+    return (uint8_t)((uint32_t)i & 0xffu);
+}
+void orc_surface_u8(const double* rgb, size_t npx, uint8_t* out) {
+    for (size_t k = 0; k < 3 * npx; k++) out[k] = surface_byte(rgb[k]);
+}

@@ -58,6 +58,12 @@ int orc_synthetic_scene(int n_spheres, int n_walls, uint64_t seed, rt_prim* out,
 /* The reference scene of main.cpp:160-163 (1 sphere + 2 walls). Returns 3. */
 int orc_default_scene(rt_prim* out, double* raw_normals);
 
+/* main.cpp:345's surface bytes: SDL_MapRGB(fmt, val.x*255, ...) converts each double to
+ * its Uint8 parameter implicitly; on the reference's x86-64 build that is cvttsd2si
+ * (int32 toward zero; NaN / out of range -> INT32_MIN) then the low byte.  npx pixels of
+ * 3 doubles -> 3 bytes each. */
+void orc_surface_u8(const double* rgb, size_t npx, uint8_t* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -84,6 +84,15 @@ struct rt_ctx {
     void* d_out = nullptr;
     size_t d_out_cap = 0;
     unsigned long long* d_segs = nullptr;
+    // Renders enqueued on caller streams (rt_render_device): per stream, an event recorded
+    // behind its latest launch.  rt_set_scene and rt_ctx_destroy wait on every one of them
+    // before they overwrite or free the device scene, so a frame still in flight on a
+    // non-blocking stream never reads a half-replaced scene.
+    struct Inflight {
+        hipStream_t stream;
+        hipEvent_t ev;
+    };
+    std::vector<Inflight> inflight;
     char last_err[256] = {0};
 };
 
@@ -100,6 +109,61 @@ int hip_fail(rt_ctx* ctx, hipError_t e, const char* what) {
         hipError_t e_ = (call);                             \
         if (e_ != hipSuccess) return hip_fail(ctx, e_, #call); \
     } while (0)
+
+/* Makes the ctx's device current for the duration of an entry point and restores the
+ * caller's current device on every return path (the boundary must not change it). */
+struct DeviceGuard {
+    int prev = -1;
+    hipError_t err = hipSuccess;
+    explicit DeviceGuard(int device) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != device) err = hipSetDevice(device);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+    DeviceGuard(const DeviceGuard&) = delete;
+    DeviceGuard& operator=(const DeviceGuard&) = delete;
+};
+
+/* Before a launch on `st` (a caller stream): the stream's in-flight event, which the
+ * launch signals on completion (rt::launch_trace's done_event); null for ctx->stream. */
+#ifndef RT_TRACK_STREAMS
+#define RT_TRACK_STREAMS 1
+#endif
+int launch_event(rt_ctx* ctx, hipStream_t st, hipEvent_t* ev) {
+    *ev = nullptr;
+    if (!RT_TRACK_STREAMS || st == ctx->stream) return RT_OK;  // rt_set_scene syncs ctx->stream
+    for (auto& f : ctx->inflight)
+        if (f.stream == st) {
+            *ev = f.ev;
+            return RT_OK;
+        }
+    constexpr size_t kMaxStreams = 16;
+    if (ctx->inflight.size() >= kMaxStreams) {
+        // many distinct streams: retire the oldest entry (wait for its frame) and reuse it
+        rt_ctx::Inflight f = ctx->inflight.front();
+        RT_HIP(ctx, hipEventSynchronize(f.ev));
+        ctx->inflight.erase(ctx->inflight.begin());
+        f.stream = st;
+        ctx->inflight.push_back(f);
+        *ev = f.ev;
+        return RT_OK;
+    }
+    rt_ctx::Inflight f{st, nullptr};
+    RT_HIP(ctx, hipEventCreate(&f.ev));
+    ctx->inflight.push_back(f);
+    *ev = f.ev;
+    return RT_OK;
+}
+
+/* Every render this ctx has enqueued, on any stream, has finished. */
+int wait_inflight(rt_ctx* ctx) {
+    if (ctx->stream) RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    for (auto& f : ctx->inflight) RT_HIP(ctx, hipEventSynchronize(f.ev));
+    return RT_OK;
+}
 
 /* vec.cpp restatements used to pack Wall invariants (same fp64 operations). */
 struct hv3 {
@@ -121,6 +185,7 @@ int bytes_per_pixel(int32_t f) {
         case RT_OUT_RGB_F32: return 12;
         case RT_OUT_RGB_F64: return 24;
         case RT_OUT_RGBA8: return 4;
+        case RT_OUT_RGBA8_WRAP: return 4;
         default: return 0;
     }
 }
@@ -723,9 +788,10 @@ int rt_ctx_create(int device, rt_ctx** out) {
     if (!ctx) return RT_ERR_OUT_OF_MEMORY;
     ctx->device = device;
     int st = RT_OK;
+    DeviceGuard dg(device);
     do {
         hipError_t e;
-        if ((e = hipSetDevice(device)) != hipSuccess) { st = hip_fail(ctx, e, "hipSetDevice"); break; }
+        if ((e = dg.err) != hipSuccess) { st = hip_fail(ctx, e, "hipSetDevice"); break; }
         if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess) {
             st = hip_fail(ctx, e, "hipStreamCreate"); break;
         }
@@ -748,8 +814,10 @@ int rt_ctx_create(int device, rt_ctx** out) {
 
 int rt_ctx_destroy(rt_ctx* ctx) {
     if (!ctx) return RT_ERR_INVALID_ARG;
-    (void)hipSetDevice(ctx->device);
-    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    DeviceGuard dg(ctx->device);
+    (void)wait_inflight(ctx);  // frames in flight on caller streams still read the scene
+    for (auto& f : ctx->inflight) (void)hipEventDestroy(f.ev);
+    ctx->inflight.clear();
     if (ctx->d_scene) (void)hipFree(ctx->d_scene);
     if (ctx->d_out) (void)hipFree(ctx->d_out);
     if (ctx->d_segs) (void)hipFree(ctx->d_segs);
@@ -769,8 +837,11 @@ int rt_set_scene(rt_ctx* ctx, const rt_prim* prims, int32_t n) {
     rt_ctx::SceneHost sc;
     const int st = pack_scene(prims, n, sc);
     if (st != RT_OK) return st;
-    RT_HIP(ctx, hipSetDevice(ctx->device));
-    RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    DeviceGuard dg(ctx->device);
+    RT_HIP(ctx, dg.err);
+    // no render of the old scene may still be running, on the ctx's stream or a caller's
+    const int ws = wait_inflight(ctx);
+    if (ws != RT_OK) return ws;
     if (sc.total > ctx->scene_bytes) {
         if (ctx->d_scene) RT_HIP(ctx, hipFree(ctx->d_scene));
         ctx->d_scene = nullptr;
@@ -856,7 +927,8 @@ int rt_set_option(rt_ctx* ctx, int32_t option, int64_t value) {
 
 int rt_selftest(rt_ctx* ctx, int32_t test, uint64_t n, uint64_t seed, uint64_t* mismatches) {
     if (!ctx || !mismatches || test < 0 || test > 2) return RT_ERR_INVALID_ARG;
-    RT_HIP(ctx, hipSetDevice(ctx->device));
+    DeviceGuard dg(ctx->device);
+    RT_HIP(ctx, dg.err);
     RT_HIP(ctx, hipMemsetAsync(ctx->d_segs, 0, sizeof(unsigned long long), ctx->stream));
     const int e = rt::launch_selftest(test, n, seed, ctx->d_segs, ctx->stream);
     if (e != (int)hipSuccess) return hip_fail(ctx, (hipError_t)e, "launch k_selftest");
@@ -986,13 +1058,20 @@ int rt_render_device(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nr
     int st = check_render_args(ctx, cam, row0, nrows, depth, precision, out_format);
     if (st != RT_OK) return st;
     if (!d_out && nrows > 0 && cam->width > 0) return RT_ERR_INVALID_ARG;
+    // the ctx's buffers (row feedback) and the launch belong to ctx->device, whatever
+    // device the caller has current
+    DeviceGuard dg(ctx->device);
+    RT_HIP(ctx, dg.err);
     rt::KParams p = make_params(ctx, cam, row0, nrows, depth, flags, out_format, d_out,
                                 reinterpret_cast<unsigned long long*>(d_segments));
     void* s = stream ? stream : static_cast<void*>(ctx->stream);
     hipStream_t hs = static_cast<hipStream_t>(s);
     st = prepare_rows(ctx, cam, row0, nrows, hs, p);
     if (st != RT_OK) return st;
-    const int e = rt::launch_trace(p, precision, s);
+    hipEvent_t done = nullptr;
+    st = launch_event(ctx, hs, &done);
+    if (st != RT_OK) return st;
+    const int e = rt::launch_trace(p, precision, s, done);
     if (e != (int)hipSuccess) return hip_fail(ctx, (hipError_t)e, "launch k_trace");
     return snapshot_costs(ctx, cam, row0, nrows, hs, p);
 }
@@ -1004,7 +1083,8 @@ int rt_render(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nrows, in
     if (st != RT_OK) return st;
     const size_t bytes = (size_t)nrows * (size_t)cam->width * (size_t)bytes_per_pixel(out_format);
     if (!out && bytes > 0) return RT_ERR_INVALID_ARG;
-    RT_HIP(ctx, hipSetDevice(ctx->device));
+    DeviceGuard dg(ctx->device);
+    RT_HIP(ctx, dg.err);
     if (bytes > ctx->d_out_cap) {
         RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
         if (ctx->d_out) RT_HIP(ctx, hipFree(ctx->d_out));

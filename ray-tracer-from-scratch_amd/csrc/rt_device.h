@@ -59,7 +59,7 @@ static_assert(sizeof(DevMat) == 64, "material layout");
 static_assert(sizeof(DevMat32) == 32, "material layout");
 
 enum { PREC_F64 = 0, PREC_F32 = 1, PREC_MIXED = 2, PREC_PATH64 = 3 };
-enum { OUT_RGB_F32 = 0, OUT_RGB_F64 = 1, OUT_RGBA8 = 2 };
+enum { OUT_RGB_F32 = 0, OUT_RGB_F64 = 1, OUT_RGBA8 = 2, OUT_RGBA8_WRAP = 3 };
 enum { FLAG_SUN = 1 };
 
 // Pixel tile of one workgroup: RT_WAVES_PER_BLOCK waves (1, 2 or 4), each an 8x8 square.
@@ -164,8 +164,10 @@ struct KParams {
 // kernarg_stale.hip: consistent across back-to-back launches)
 static_assert(sizeof(KParams) <= 16384, "kernel arguments over 16 KB");
 
-// Host-side launchers (rt_trace.hip).  Return a hipError_t as int.
-int launch_trace(const KParams& p, int prec, void* stream);
+// Host-side launchers (rt_trace.hip).  Return a hipError_t as int.  done_event (a
+// hipEvent_t, may be null) is signalled by the kernel's own completion (hipExtLaunchKernel
+// stop event: no separate marker packet, unlike a hipEventRecord behind the launch).
+int launch_trace(const KParams& p, int prec, void* stream, void* done_event = nullptr);
 int max_depth();
 // Device self-test of the exact fp64 helpers against IEEE operations:
 // which 0 = division (shared reciprocal), 1 = integer-exponent pow vs pow(),

@@ -38,6 +38,7 @@
  * register stack indexed by the wave-uniform bounce counter; the stack is unwound in
  * reverse with the same operations, so local = color*s is recomputed bit-identically.
  */
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <float.h>
@@ -1400,6 +1401,13 @@ __device__ __forceinline__ unsigned q8(double v) {
     v = v < 1.0 ? v : 1.0;
     return (unsigned)(v * 255.0);
 }
+/* RGBA8_WRAP: the reference's x86-64 bytes for every value — cvttsd2si of v*255 (int32,
+ * toward zero; NaN and |v*255| >= 2^31 give 0x80000000), then the low byte. */
+__device__ __forceinline__ unsigned q8_wrap(double v) {
+    const double t = v * 255.0;
+    const int i = (t > -2147483649.0 && t < 2147483648.0) ? (int)t : (int)0x80000000u;
+    return (unsigned)i & 0xffu;
+}
 
 __device__ __forceinline__ void store_px(const KParams& p, size_t px, double cr, double cg,
                                          double cb) {
@@ -1413,8 +1421,11 @@ __device__ __forceinline__ void store_px(const KParams& p, size_t px, double cr,
         o[0] = cr;
         o[1] = cg;
         o[2] = cb;
-    } else {
+    } else if (p.outf == OUT_RGBA8) {
         const unsigned v = q8(cr) | (q8(cg) << 8) | (q8(cb) << 16) | (255u << 24);
+        static_cast<unsigned*>(p.out)[px] = v;
+    } else {
+        const unsigned v = q8_wrap(cr) | (q8_wrap(cg) << 8) | (q8_wrap(cb) << 16) | (255u << 24);
         static_cast<unsigned*>(p.out)[px] = v;
     }
 }
@@ -1547,38 +1558,42 @@ k_trace(KParams p) {
 #endif
 }
 
-template <int PREC, bool SUN, bool INT_EXP, bool CULL>
-static hipError_t launch_depth(const KParams& p, dim3 grid, hipStream_t st) {
-    if (p.depth <= MAXD_SMALL)
-        hipLaunchKernelGGL((k_trace<PREC, SUN, INT_EXP, CULL, MAXD_SMALL>), grid, dim3(BLOCK), 0,
-                           st, p);
-    else if (p.depth <= MAXD_MID)
-        hipLaunchKernelGGL((k_trace<PREC, SUN, INT_EXP, CULL, MAXD_MID>), grid, dim3(BLOCK), 0, st,
-                           p);
-    else if (p.depth <= MAXD_REF)
-        hipLaunchKernelGGL((k_trace<PREC, SUN, INT_EXP, CULL, MAXD_REF>), grid, dim3(BLOCK), 0, st,
-                           p);
+template <int PREC, bool SUN, bool INT_EXP, bool CULL, int MAXD>
+static void launch_one(const KParams& p, dim3 grid, hipStream_t st, hipEvent_t done) {
+    if (done)
+        hipExtLaunchKernelGGL((k_trace<PREC, SUN, INT_EXP, CULL, MAXD>), grid, dim3(BLOCK), 0, st,
+                              nullptr, done, 0, p);
     else
-        hipLaunchKernelGGL((k_trace<PREC, SUN, INT_EXP, CULL, MAXD_LARGE>), grid, dim3(BLOCK), 0,
-                           st, p);
+        hipLaunchKernelGGL((k_trace<PREC, SUN, INT_EXP, CULL, MAXD>), grid, dim3(BLOCK), 0, st, p);
+}
+template <int PREC, bool SUN, bool INT_EXP, bool CULL>
+static hipError_t launch_depth(const KParams& p, dim3 grid, hipStream_t st, hipEvent_t done) {
+    if (p.depth <= MAXD_SMALL)
+        launch_one<PREC, SUN, INT_EXP, CULL, MAXD_SMALL>(p, grid, st, done);
+    else if (p.depth <= MAXD_MID)
+        launch_one<PREC, SUN, INT_EXP, CULL, MAXD_MID>(p, grid, st, done);
+    else if (p.depth <= MAXD_REF)
+        launch_one<PREC, SUN, INT_EXP, CULL, MAXD_REF>(p, grid, st, done);
+    else
+        launch_one<PREC, SUN, INT_EXP, CULL, MAXD_LARGE>(p, grid, st, done);
     return hipGetLastError();
 }
 template <int PREC, bool SUN, bool INT_EXP>
-static hipError_t launch_cull(const KParams& p, dim3 grid, hipStream_t st) {
-    return p.wave_cull ? launch_depth<PREC, SUN, INT_EXP, true>(p, grid, st)
-                       : launch_depth<PREC, SUN, INT_EXP, false>(p, grid, st);
+static hipError_t launch_cull(const KParams& p, dim3 grid, hipStream_t st, hipEvent_t done) {
+    return p.wave_cull ? launch_depth<PREC, SUN, INT_EXP, true>(p, grid, st, done)
+                       : launch_depth<PREC, SUN, INT_EXP, false>(p, grid, st, done);
 }
 template <int PREC>
-static hipError_t launch_prec(const KParams& p, dim3 grid, hipStream_t st) {
+static hipError_t launch_prec(const KParams& p, dim3 grid, hipStream_t st, hipEvent_t done) {
     if constexpr (PREC == PREC_F64 || PREC == PREC_MIXED) {
         if (p.flags & FLAG_SUN)
-            return p.int_exp ? launch_cull<PREC, true, true>(p, grid, st)
-                             : launch_cull<PREC, true, false>(p, grid, st);
-        return p.int_exp ? launch_cull<PREC, false, true>(p, grid, st)
-                         : launch_cull<PREC, false, false>(p, grid, st);
+            return p.int_exp ? launch_cull<PREC, true, true>(p, grid, st, done)
+                             : launch_cull<PREC, true, false>(p, grid, st, done);
+        return p.int_exp ? launch_cull<PREC, false, true>(p, grid, st, done)
+                         : launch_cull<PREC, false, false>(p, grid, st, done);
     } else {
-        return (p.flags & FLAG_SUN) ? launch_cull<PREC, true, true>(p, grid, st)
-                                    : launch_cull<PREC, false, true>(p, grid, st);
+        return (p.flags & FLAG_SUN) ? launch_cull<PREC, true, true>(p, grid, st, done)
+                                    : launch_cull<PREC, false, true>(p, grid, st, done);
     }
 }
 
@@ -1593,18 +1608,19 @@ extern "C" int rt_diag_read(unsigned long long* out16) {
 }
 #endif
 
-int launch_trace_ns(const KParams& p, int prec, void* stream) {
+int launch_trace_ns(const KParams& p, int prec, void* stream, void* done_event) {
     if (p.W <= 0 || p.nrows <= 0) return (int)hipSuccess;
     const int ul = p.row_units_log2;
     const int units = ((p.nrows + TILE_H - 1) / TILE_H) << ul;
     const dim3 grid((((p.W + TILE_W - 1) / TILE_W) + (1 << ul) - 1) >> ul,
                     RT_TILE_PAIRS ? (units + 1) / 2 : units);
     hipStream_t st = static_cast<hipStream_t>(stream);
+    hipEvent_t done = static_cast<hipEvent_t>(done_event);
     switch (prec) {
-        case PREC_F64: return (int)launch_prec<PREC_F64>(p, grid, st);
-        case PREC_F32: return (int)launch_prec<PREC_F32>(p, grid, st);
-        case PREC_MIXED: return (int)launch_prec<PREC_MIXED>(p, grid, st);
-        case PREC_PATH64: return (int)launch_prec<PREC_PATH64>(p, grid, st);
+        case PREC_F64: return (int)launch_prec<PREC_F64>(p, grid, st, done);
+        case PREC_F32: return (int)launch_prec<PREC_F32>(p, grid, st, done);
+        case PREC_MIXED: return (int)launch_prec<PREC_MIXED>(p, grid, st, done);
+        case PREC_PATH64: return (int)launch_prec<PREC_PATH64>(p, grid, st, done);
         default: return (int)hipErrorInvalidValue;
     }
 }
@@ -1669,14 +1685,14 @@ int launch_selftest_ns(int which, uint64_t n, uint64_t seed, unsigned long long*
 }  // namespace kno / kst
 
 #if RT_STAMP
-int launch_trace_stamped(const KParams& p, int prec, void* stream) {
-    return kst::launch_trace_ns(p, prec, stream);
+int launch_trace_stamped(const KParams& p, int prec, void* stream, void* done_event) {
+    return kst::launch_trace_ns(p, prec, stream, done_event);
 }
 #else
-int launch_trace_stamped(const KParams& p, int prec, void* stream);  // rt_trace_stamp.hip
-int launch_trace(const KParams& p, int prec, void* stream) {
-    return p.tile_cost != nullptr ? launch_trace_stamped(p, prec, stream)
-                                  : kno::launch_trace_ns(p, prec, stream);
+int launch_trace_stamped(const KParams& p, int prec, void* stream, void* done_event);  // rt_trace_stamp.hip
+int launch_trace(const KParams& p, int prec, void* stream, void* done_event) {
+    return p.tile_cost != nullptr ? launch_trace_stamped(p, prec, stream, done_event)
+                                  : kno::launch_trace_ns(p, prec, stream, done_event);
 }
 int max_depth() { return kno::max_depth_ns(); }
 int launch_selftest(int which, uint64_t n, uint64_t seed, unsigned long long* d_bad,

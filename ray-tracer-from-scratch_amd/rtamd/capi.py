@@ -40,6 +40,7 @@ PRECISIONS = {"f64": RT_PREC_F64, "f32": RT_PREC_F32, "mixed": RT_PREC_MIXED,
 RT_OUT_RGB_F32 = 0
 RT_OUT_RGB_F64 = 1
 RT_OUT_RGBA8 = 2
+RT_OUT_RGBA8_WRAP = 3
 
 RT_FLAG_SUN = 1
 
@@ -210,7 +211,7 @@ def out_dtype_shape(out_format: int, nrows: int, width: int):
         return np.float32, (nrows, width, 3)
     if out_format == RT_OUT_RGB_F64:
         return np.float64, (nrows, width, 3)
-    if out_format == RT_OUT_RGBA8:
+    if out_format in (RT_OUT_RGBA8, RT_OUT_RGBA8_WRAP):
         return np.uint8, (nrows, width, 4)
     raise ValueError(out_format)
 

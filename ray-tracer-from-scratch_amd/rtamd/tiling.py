@@ -124,7 +124,14 @@ def render_tiled(renderer: "capi.Renderer", cam, depth: int, precision: int = ca
     st = stream or torch.cuda.current_stream(dev)
 
     def band(row0, nrows, out):
+        cur = torch.cuda.current_stream(dev)
+        if st != cur:
+            st.wait_stream(cur)  # the band buffer was produced on the current stream
         renderer.render_device(cam, depth, out.data_ptr(), precision, flags, out_format,
                                row0=row0, nrows=nrows, stream=st.cuda_stream)
+        if st != cur:
+            # ProcessGroupNCCL orders the gather after the CURRENT stream only: make it wait
+            # for the band's kernel on the caller's stream
+            cur.wait_stream(st)
 
     return gather_frame(band, cam.height, cam.width, shape[-1], tdtype, dev, group, dst)

@@ -63,3 +63,9 @@ def scene_by_name(name: str):
         "s64w6": lambda: scenes.synthetic_scene(64, 6),
         "s256w0": lambda: scenes.synthetic_scene(256, 0),
     }[name]()
+
+
+@pytest.fixture(scope="session")
+def golden_surface():
+    import numpy as np
+    return np.load(os.path.join(GOLDEN, "surface.npz"))

@@ -11,8 +11,11 @@ oracle/ref_harness.cpp and writes DATA only (inputs + expected outputs):
   tests/golden/frames.npz     fp64 frames rendered by the reference's recursive_ray_tracing
                               (rt_scene's loop; depth 10 = rt_scene itself), small sizes
   tests/golden/rays.npz       single-ray traces (random origins/directions, all depths)
+  tests/golden/surface.npz    main.cpp:345's surface bytes (SDL_MapRGB(val*255) through its
+                              implicit double->Uint8 conversion, g++ -O3 x86-64) of every
+                              frame in frames.npz, plus edge values (wrap above 1.0, NaN)
 
-Usage:  python tests/golden/make_golden.py
+Usage:  python tests/golden/make_golden.py [--only surface]
 """
 from __future__ import annotations
 
@@ -46,9 +49,23 @@ def f(x):
     return float(x)
 
 
+def make_surface(ref) -> None:
+    """Surface bytes of the committed frames (inputs = frames.npz) and of edge values."""
+    frames = np.load(os.path.join(HERE, "frames.npz"))
+    out = {k: ref.surface_u8(frames[k]) for k in frames.files}
+    edge = np.array([[0.0, 0.5, 1.0], [1.0001, 1.084, 1.3423], [2.0, 1.0 + 1 / 255, -0.001],
+                     [-1.5, np.nan, 1e12], [0.999999, 255.0 / 255, 3.99]], np.float64)
+    out["edge__in"] = edge
+    out["edge__u8"] = ref.surface_u8(edge)
+    np.savez_compressed(os.path.join(HERE, "surface.npz"), **out)
+
+
 def main() -> None:
     orc_mod.build(ref=True)
     ref = orc_mod.Reference()
+    if "--only" in sys.argv and sys.argv[sys.argv.index("--only") + 1] == "surface":
+        make_surface(ref)
+        return
     L = ref.lib
     A = orc_mod._arr
     kat: dict = {"source": "reference vec.cpp/scene.cpp/main.cpp:1-139 compiled by oracle/Makefile"}
@@ -185,6 +202,7 @@ def main() -> None:
         rays[f"{scene_name}__depth"] = depth
         rays[f"{scene_name}__rgb"] = rgb
     np.savez_compressed(os.path.join(HERE, "rays.npz"), **rays)
+    make_surface(ref)
     print("wrote", sorted(os.listdir(HERE)))
 
 

@@ -116,6 +116,81 @@ def test_rgba8_epilogue(rend, oracle):
     assert ok.all()
 
 
+def test_rgba8_wrap_matches_reference_surface_bytes(rend, golden_frames, golden_surface):
+    """RT_OUT_RGBA8_WRAP = main.cpp:345's bytes as the reference's x86-64 build makes them
+    (tests/golden/surface.npz, recorded from the compiled conversion): highlights above 1.0
+    wrap mod 256.  F64 renders agree with the reference to <= 1e-12, so a byte may differ
+    only where v*255 sits on an integer boundary."""
+    wrapped = 0
+    for key in golden_frames.files:
+        name, w, h, depth = parse_frame_key(key)
+        img, _, _ = render(rend, scene_by_name(name), w, h, depth, capi.RT_PREC_F64,
+                           fmt=capi.RT_OUT_RGBA8_WRAP)
+        ref64, exp = golden_frames[key], golden_surface[key]
+        assert (img[..., 3] == 255).all(), key
+        t = ref64 * 255.0
+        edge = np.abs(t - np.round(t)) < 1e-9
+        assert ((img[..., :3] == exp) | edge).all(), key
+        wrapped += int(((ref64 > 1.0) & ~edge).sum())
+        # RT_OUT_RGBA8 is the same bytes where the reference is in range, 255 above it
+        sat, _, _ = render(rend, scene_by_name(name), w, h, depth, capi.RT_PREC_F64,
+                           fmt=capi.RT_OUT_RGBA8)
+        inr = (ref64 >= 0) & (ref64 <= 1.0) & ~edge
+        assert (sat[..., :3][inr] == exp[inr]).all(), key
+        assert (sat[..., :3][(ref64 > 1.0) & ~edge] == 255).all(), key
+    assert wrapped > 100   # the out-of-range behaviour is exercised, not just truncation
+
+
+def test_set_scene_waits_for_renders_on_caller_streams(rend):
+    """rt_set_scene must not overwrite the device scene under frames still in flight on a
+    non-blocking caller stream: queue heavy frames of scene A on a torch
+    stream, swap to scene B at once, and every queued frame is still scene A's."""
+    import torch
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.Stream(dev)
+    sa, sb = scenes.synthetic_scene(64, 6), scenes.synthetic_scene(64, 6, seed=99)
+    rend.set_scene(scenes.to_prims(sa))
+    cam = capi.camera_init(**scenes.camera_args(1920, 1080))
+    ref, _ = rend.render(cam, 6, capi.RT_PREC_F64, 0, capi.RT_OUT_RGB_F32)
+    outs = [torch.full((1080, 1920, 3), -1.0, device=dev) for _ in range(4)]
+    torch.cuda.synchronize()
+    for o in outs:
+        rend.render_device(cam, 6, o.data_ptr(), capi.RT_PREC_F64, 0, capi.RT_OUT_RGB_F32,
+                           stream=st.cuda_stream)
+    rend.set_scene(scenes.to_prims(sb))   # frames above may still be running
+    torch.cuda.synchronize()
+    for o in outs:
+        assert np.array_equal(o.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+    other, _ = rend.render(cam, 6, capi.RT_PREC_F64, 0, capi.RT_OUT_RGB_F32)
+    assert not np.array_equal(other, ref)
+
+
+def test_calls_keep_the_callers_current_device_and_contexts_are_independent(rend):
+    """Entry points run on the ctx's device and restore the caller's current device; two
+    contexts interleaved on different streams render their own scenes."""
+    import torch
+    dev = torch.device("cuda", 0)
+    before = torch.cuda.current_device()
+    sa, sb = scenes.synthetic_scene(8, 4), scenes.default_scene()
+    cam = capi.camera_init(**scenes.camera_args(160, 90))
+    with capi.Renderer(0) as r2:
+        rend.set_scene(scenes.to_prims(sa))
+        r2.set_scene(scenes.to_prims(sb))
+        ra, _ = rend.render(cam, 4, capi.RT_PREC_PATH64, 0, capi.RT_OUT_RGB_F32)
+        rb, _ = r2.render(cam, 4, capi.RT_PREC_PATH64, 0, capi.RT_OUT_RGB_F32)
+        s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+        oa = [torch.empty((90, 160, 3), device=dev) for _ in range(3)]
+        ob = [torch.empty((90, 160, 3), device=dev) for _ in range(3)]
+        torch.cuda.synchronize()
+        for a, b in zip(oa, ob):
+            rend.render_device(cam, 4, a.data_ptr(), capi.RT_PREC_PATH64, stream=s1.cuda_stream)
+            r2.render_device(cam, 4, b.data_ptr(), capi.RT_PREC_PATH64, stream=s2.cuda_stream)
+        torch.cuda.synchronize()
+        for a, b in zip(oa, ob):
+            assert np.array_equal(a.cpu().numpy(), ra) and np.array_equal(b.cpu().numpy(), rb)
+    assert torch.cuda.current_device() == before
+
+
 # ---------------------------------------------------------------- semantics
 def test_segment_count_matches_oracle(rend, oracle):
     for sc, depth in ((scenes.default_scene(), 10), (scenes.synthetic_scene(8, 4), 4),
@@ -578,5 +653,15 @@ def test_render_tiled_rccl_single_rank(rend):
         torch.cuda.synchronize()
         ref, _ = rend.render(cam, 4, capi.RT_PREC_PATH64, 0, capi.RT_OUT_RGB_F32)
         assert np.array_equal(frame.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+        # an explicit stream that is NOT the current one: the gather (ordered after the
+        # current stream by ProcessGroupNCCL) must still see the finished band
+        big = capi.camera_init(**scenes.camera_args(1920, 1080))
+        rend.set_scene(scenes.to_prims(scenes.synthetic_scene(64, 6)))
+        side = torch.cuda.Stream()
+        assert side != torch.cuda.current_stream()
+        frame = tiling.render_tiled(rend, big, 6, capi.RT_PREC_F64, stream=side)
+        got = frame.cpu().numpy()
+        ref, _ = rend.render(big, 6, capi.RT_PREC_F64, 0, capi.RT_OUT_RGB_F32)
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
     finally:
         dist.destroy_process_group()

@@ -161,3 +161,26 @@ def test_against_live_reference_random_scenes(oracle):
         for depth in (0, 3, 7):
             o64, _, _ = oracle.render(prims, cam, depth)
             assert _same(o64, ref.render(prims, raw, ca, depth)), (seed, depth)
+
+
+def test_surface_bytes_match_reference_conversion(oracle, golden_frames, golden_surface):
+    """main.cpp:345's implicit double->Uint8 (the reference's x86-64 build: truncation,
+    highlights above 1.0 wrap mod 256, NaN -> 0) restated in the oracle equals the bytes
+    recorded from that conversion compiled by g++ (tests/golden/surface.npz)."""
+    for key in golden_frames.files:
+        assert np.array_equal(oracle.surface_u8(golden_frames[key]), golden_surface[key]), key
+    assert np.array_equal(oracle.surface_u8(golden_surface["edge__in"]), golden_surface["edge__u8"])
+    # the fixtures hold out-of-range pixels, so the wrap is pinned, not just truncation
+    over = sum(int((golden_frames[k] > 1.0).sum()) for k in golden_frames.files)
+    assert over > 100
+    assert golden_surface["edge__u8"][1].tolist() == [255, 20, 86]
+
+
+@pytest.mark.skipif(not __import__("oracle").Reference.available(),
+                    reason="reference build only exists where /root/reference does")
+def test_surface_bytes_live_reference(oracle):
+    import oracle as orc_mod
+    ref = orc_mod.Reference()
+    rng = np.random.default_rng(5)
+    v = np.concatenate([rng.uniform(-3, 3, (4000, 3)), rng.uniform(0, 1.5, (4000, 3))])
+    assert np.array_equal(oracle.surface_u8(v), ref.surface_u8(v))
