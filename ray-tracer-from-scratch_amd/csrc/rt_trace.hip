@@ -61,6 +61,9 @@
 #ifndef RT_LAZY_TERMS      // PATH64: |d|^2, 1/|d|^2, |d| only when a sphere test or a
 #define RT_LAZY_TERMS 0    // reflection needs them (wave-uniform; A/B: +2% at c2, off)
 #endif
+#ifndef RT_SKY_FAST        // PATH64 linear scan: a tile whose keep mask is empty (no primitive's
+#define RT_SKY_FAST 1      // pixel box meets it: every primary ray misses) shades its sky/ground
+#endif                     // at once, without |d|^2, 1/|d|^2, |d| or the bounce loop
 #ifndef RT_BOX_SCHED_BARRIER
 #define RT_BOX_SCHED_BARRIER 1
 #endif
@@ -72,6 +75,16 @@
 #endif
 #ifndef RT_WAVE_TIMES      // diagnostic build: per-wave start/end stamps into KParams::stats
 #define RT_WAVE_TIMES 0    // (tools/wave_times.py); never on in the product
+#endif
+#ifndef RT_STAGE_TIMES     // diagnostic build: shader-clock stamps at stage boundaries of every
+#define RT_STAGE_TIMES 0   // wave into KParams::stats (tools/stage_times.py); never in the product
+#endif
+#if RT_STAGE_TIMES
+#define STAGE(i) (g_stage[(i)] = __builtin_amdgcn_s_memtime())
+#else
+#define STAGE(i) \
+    do {         \
+    } while (0)
 #endif
 #ifndef RT_DIAG            // diagnostic build: count wave/lane entries of branch bodies
 #define RT_DIAG 0          // into g_diag (rt_diag_read); never on in the product
@@ -810,6 +823,16 @@ __device__ __forceinline__ f3 local_color_f(const DevMat32& m, float s, float ks
 }
 __device__ __forceinline__ f3 tof(d3 v) { return F3((float)v.x, (float)v.y, (float)v.z); }
 
+/* PATH64's terminal miss (out_color, main.cpp:28-37) in fp32: ground below the horizon by
+ * the exact direction's sign, else the sky lerp at normalize(d).z^0.25. */
+__device__ __forceinline__ f3 sky32(const d3& d) {
+    const f3 nv32 = fnormalize(tof(d));
+    if (d.z < 0.0) return F3(0.025f, 0.05f, 0.075f);
+    const float tz = fsqrt(fsqrt(nv32.z));
+    return F3(fmaf(tz, 0.14f - 0.36f, 0.36f), fmaf(tz, 0.21f - 0.45f, 0.45f),
+              fmaf(tz, 0.49f - 0.57f, 0.57f));
+}
+
 /* Dispatch order of tile rows (workgroup row blockIdx.y -> tile row).  Per-tile cost is
  * very uneven (sky/ground tiles end after one segment, tiles over reflective walls bounce
  * to full depth), and a heavy wave dispatched late ends the kernel long after the last
@@ -992,7 +1015,8 @@ __device__ __forceinline__ HitD scan_d(const KParams& p, const RayD& r, bool ali
  * MIXED, the parity modes); otherwise in fp32 (PATH64). */
 template <bool MIXED, bool COLOR64, bool SUN, bool INT_EXP, bool CULL, int MAXD>
 __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool alive,
-                                            int& segs, uint64_t& t_start, uint64_t braw_in) {
+                                            int& segs, uint64_t& t_start, uint64_t braw_in,
+                                            uint64_t* g_stage = nullptr) {
     using CT = typename std::conditional<COLOR64, double, float>::type;
     const d3 cpos = ld3(p.pos);
     const d3 pc = (ld3(p.tl) + ld3(p.dx) * (double)x) + ld3(p.dy) * (double)i;  // main.cpp:132
@@ -1001,8 +1025,10 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
     // main.cpp:133-134 (direction not normalised); the sphere terms only where needed
     // (PATH64: the fp32 terminal segment needs none of them)
     constexpr bool LAZY = RT_LAZY_TERMS && !COLOR64 && !CULL && RT_TERMINAL_F32;
-    RayD r = LAZY ? make_ray_lazy(cpos, cpos - pc) : make_ray(cpos, cpos - pc);
+    constexpr bool SKYF = RT_SKY_FAST && !COLOR64 && !CULL && RT_TERMINAL_F32;
+    RayD r = (LAZY || SKYF) ? make_ray_lazy(cpos, cpos - pc) : make_ray(cpos, cpos - pc);
     bool terms = !LAZY;
+    STAGE(1);
     constexpr bool sun = SUN;
     // the wave's start stamp for the dispatch-order feedback (stamped build only): here,
     // between ray generation and the box compare's wait on its load
@@ -1011,6 +1037,21 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
     const TileO tile = tile_origin(x, i);
     uint64_t keep = CULL ? ~0ull : box_keep(braw, tile);  // all lanes active
     if (p.nbox == 0) keep = ~0ull;
+    STAGE(6);
+    if (SKYF) {
+        if (keep == 0) {  // wave-uniform: every primary ray of the tile misses (tile bins)
+            f3 c = F3(0.f, 0.f, 0.f);
+            if (alive) {
+                ++segs;
+                c = sky32(r.d);
+            }
+            STAGE(2);
+            STAGE(3);
+            STAGE(4);
+            return D3(c.x, c.y, c.z);
+        }
+        if (!LAZY) ray_terms(r);
+    }
     const uint64_t smask = p.nS >= 64 ? ~0ull : (1ull << p.nS) - 1;
 
     CT st_s[MAXD];
@@ -1044,6 +1085,7 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
         }
 #endif
         const HitD h = scan_d<MIXED, CULL>(p, r, alive, k == 0, km != ~0ull, km);
+        if (k == 0) STAGE(2);
         const bool last = k >= p.depth || k >= MAXD;  // remaining_iterations <= 0 (main.cpp:105)
         if (LAZY && !terms && __any(alive && !last && h.slot >= 0)) {  // a reflection follows
             ray_terms(r);
@@ -1054,17 +1096,10 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
         if (!COLOR64 && RT_TERMINAL_F32 && (last || h.slot < 0)) {
             // PATH64, last segment of the path: nothing here feeds another ray
             DIAG(10);
-            const f3 d32 = tof(r.d);
-            const f3 nv32 = fnormalize(d32);
             if (h.slot < 0) {
-                if (r.d.z < 0.0) {
-                    c32 = F3(0.025f, 0.05f, 0.075f);
-                } else {
-                    const float tz = fsqrt(fsqrt(nv32.z));
-                    c32 = F3(fmaf(tz, 0.14f - 0.36f, 0.36f), fmaf(tz, 0.21f - 0.45f, 0.45f),
-                             fmaf(tz, 0.49f - 0.57f, 0.57f));
-                }
+                c32 = sky32(r.d);
             } else {
+                const f3 nv32 = fnormalize(tof(r.d));
                 const d3 pos = r.o + r.d * h.dist;
                 f3 N32;
                 if (h.slot < p.nS) {
@@ -1140,6 +1175,7 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
             r = make_ray(pos + N * .0001, nv - nn * cc);
         }
     }
+    STAGE(3);
     for (int q = MAXD - 1; q >= 0; --q) {
         if ((!RT_UNWIND_KEND || q < kend) && q < n) {  // uniform test: levels no lane reached
             const DevMat& m = p.mat[st_m[q]];
@@ -1155,6 +1191,7 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
             }
         }
     }
+    STAGE(4);
     if (COLOR64) return c64;
     return D3(c32.x, c32.y, c32.z);
 }
@@ -1482,10 +1519,31 @@ __device__ __forceinline__ void trace_tile(const KParams& p, int bx, int trow, i
         const f3 c = trace_pixel_f<SUN, CULL, MAXD>(p, x, i, valid, segs, t_tile, braw);
         if (valid) store_pixel(p, r, x, c.x, c.y, c.z);
     } else {
+#if RT_STAGE_TIMES
+        uint64_t g_stage[8];
+        STAGE(0);
+        const d3 c =
+            trace_pixel_d<PREC == PREC_MIXED, PREC != PREC_PATH64, SUN, INT_EXP, CULL, MAXD>(
+                p, x, i, valid, segs, t_tile, braw, g_stage);
+#else
         const d3 c =
             trace_pixel_d<PREC == PREC_MIXED, PREC != PREC_PATH64, SUN, INT_EXP, CULL, MAXD>(
                 p, x, i, valid, segs, t_tile, braw);
+#endif
         if (valid) store_pixel(p, r, x, c.x, c.y, c.z);
+#if RT_STAGE_TIMES
+        STAGE(5);
+        {
+            int sg = segs;
+            for (int off = 32; off > 0; off >>= 1) sg += __shfl_xor(sg, off, 64);
+            if (p.stats != nullptr && lane == 0 && bx < gx) {
+                const size_t wid = ((size_t)trow * gx + bx) * (BLOCK / 64) + wave;
+                for (int q = 0; q < 6; ++q) p.stats[8 * wid + q] = g_stage[q];
+                p.stats[8 * wid + 6] = (unsigned long long)sg;
+                p.stats[8 * wid + 7] = g_stage[6];
+            }
+        }
+#endif
     }
     count_segments(p, segs);
     if (RT_STAMP && lane == 0 && bx < gx) {

@@ -19,11 +19,14 @@ def main():
     ap.add_argument("--launches", type=int, default=10)
     ap.add_argument("--sun", action="store_true")
     ap.add_argument("--depth", type=int, default=-1, help="-1 = the config's depth")
+    ap.add_argument("--lib", default="", help="another build of librt_amd.so (A/B)")
     args = ap.parse_args()
     import torch
     dev = torch.device("cuda", 0)
     stream = torch.cuda.Stream(dev)
     cfg = scenes.CONFIGS[args.config]
+    if args.lib:
+        capi._lib = capi.load(os.path.abspath(args.lib))
     rend = capi.Renderer(0)
     rend.set_scene(scenes.to_prims(cfg.scene()))
     cam = capi.camera_init(**scenes.camera_args(cfg.width, cfg.height))
