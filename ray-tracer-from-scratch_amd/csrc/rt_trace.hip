@@ -61,7 +61,7 @@
 #ifndef RT_LAZY_TERMS      // PATH64: |d|^2, 1/|d|^2, |d| only when a sphere test or a
 #define RT_LAZY_TERMS 0    // reflection needs them (wave-uniform; A/B: +2% at c2, off)
 #endif
-#ifndef RT_SKY_FAST        // PATH64 linear scan: a tile whose keep mask is empty (no primitive's
+#ifndef RT_SKY_FAST        // PATH64/F32 linear scan: a tile whose keep mask is empty (no primitive's
 #define RT_SKY_FAST 1      // pixel box meets it: every primary ray misses) shades its sky/ground
 #endif                     // at once, without |d|^2, 1/|d|^2, |d| or the bounce loop
 #ifndef RT_BOX_SCHED_BARRIER
@@ -1303,6 +1303,22 @@ __device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, bool
 #else
     const uint64_t keep = (!CULL && p.nbox > 0) ? tile_keep(p, p.box, tile) : ~0ull;
 #endif
+    if (!CULL && RT_SKY_FAST && keep == 0) {
+        // wave-uniform: every primary ray misses (tile bins): the loop's miss shading below,
+        // operation for operation, without the loop
+        if (alive) {
+            ++segs;
+            const f3 nv = d * frsq(fdot(d, d));
+            if (d.z < 0.0f) {
+                c = F3(0.025f, 0.05f, 0.075f);
+            } else {
+                const float tz = fsqrt(fsqrt(nv.z));
+                c = F3(fmaf(tz, 0.14f - 0.36f, 0.36f), fmaf(tz, 0.21f - 0.45f, 0.45f),
+                       fmaf(tz, 0.49f - 0.57f, 0.57f));
+            }
+        }
+        return c;
+    }
     int kend = 0;  // wave-uniform: bounce iterations run (every lane's n <= kend)
     for (int k = 0;; ++k) {
         if (!__any(alive)) {
