@@ -52,6 +52,9 @@
 #ifndef RT_WALLS_FIRST
 #define RT_WALLS_FIRST 1
 #endif
+#ifndef RT_WALL_NOSIGN     // 1: the wall test forms t = num/den for every lane and keeps t > 0 and
+#define RT_WALL_NOSIGN 1   // t <= best in ONE branch, instead of a sign pre-test branch, then a
+#endif                     // t > 0 branch, then the t-skip branch (fewer exec-mask instructions)
 #ifndef RT_WALL_TSKIP      // 1: a wall whose t exceeds the current best skips its bounds
 #define RT_WALL_TSKIP 1    // test (exact: the reference's strict < rejects it anyway);
 #endif                     // fp64 paths only (the branch costs the fp32 path ~1% at c5)
@@ -173,6 +176,13 @@ __device__ __forceinline__ double div_r(double a, double b, double r) {
     const double e = __builtin_fma(-b, q, a);
     const double q1 = __builtin_fma(e, r, q);
     return a == 0.0 ? q : q1;
+}
+/* a / b for a != 0 (or where the sign of a zero quotient cannot matter): div_r without
+ * its a == 0 select. */
+__device__ __forceinline__ double div_r_nz(double a, double b, double r) {
+    const double q = a * r;
+    const double e = __builtin_fma(-b, q, a);
+    return __builtin_fma(e, r, q);
 }
 /* sqrt(x) correctly rounded: LLVM's fp64 sqrt sequence (rsq + Goldschmidt/Newton
  * refinement) without its range scaling, which is the identity for x >= 2^-767; smaller
@@ -372,11 +382,20 @@ __device__ __forceinline__ void wall_exact(const Wall64& Wl, int w, const KParam
     const d3 P = ld3(Wl.P);
     const double den = dot(n, r.d);
     const double num = EYE ? p.eye_w[w] : dot(P - r.o, n);
-    if (!((num > 0 && den > 0) || (num < 0 && den < 0))) return;
-    DIAG(4);
-    const double t = div_r(num, den, rcp_refined(den));
-    if (!(t > 0)) return;
-    if (RT_WALL_TSKIP && t > h.dist) return;  // loses to the current best either way
+    double t;
+    if (RT_WALL_NOSIGN) {
+        // t <= 0 (opposite signs or num == 0), NaN (0/0) and +-inf (den == 0: rcp_refined
+        // gives NaN) all fail t > 0, as in the reference (scene.cpp:12); the zero-quotient
+        // sign does not matter since 0 fails t > 0 either way
+        t = div_r_nz(num, den, rcp_refined(den));
+        if (!(t > 0) || (RT_WALL_TSKIP && t > h.dist)) return;  // t > best loses anyway
+    } else {
+        if (!((num > 0 && den > 0) || (num < 0 && den < 0))) return;
+        DIAG(4);
+        t = div_r(num, den, rcp_refined(den));
+        if (!(t > 0)) return;
+        if (RT_WALL_TSKIP && t > h.dist) return;  // loses to the current best either way
+    }
     DIAG(6);
     const d3 q = (r.o + r.d * t) - P;  // ray::at (scene.h:16) minus the corner
     const double px = dot(q, ld3(Wl.X));
