@@ -55,6 +55,12 @@
 #ifndef RT_WALL_NOSIGN     // 1: the wall test forms t = num/den for every lane and keeps t > 0 and
 #define RT_WALL_NOSIGN 1   // t <= best in ONE branch, instead of a sign pre-test branch, then a
 #endif                     // t > 0 branch, then the t-skip branch (fewer exec-mask instructions)
+#ifndef RT_F32_WALL_FLAT   // F32 wall test without the sign pre-test branch: one branch per wall
+#define RT_F32_WALL_FLAT 1
+#endif
+#ifndef RT_SPHERE_ONEBRANCH  // 1: Sphere::intersect's two early rejections (b > 0, det < 0)
+#define RT_SPHERE_ONEBRANCH 1  // share one branch (det/4 formed for every lane: 2 VALU)
+#endif
 #ifndef RT_WALL_TSKIP      // 1: a wall whose t exceeds the current best skips its bounds
 #define RT_WALL_TSKIP 1    // test (exact: the reference's strict < rejects it anyway);
 #endif                     // fp64 paths only (the branch costs the fp32 path ~1% at c5)
@@ -342,9 +348,13 @@ __device__ __forceinline__ void sphere_exact_oc(const d3 oc, const double c, int
                                                 const RayD& r, HitD& h,
                                                 const KParams* p = nullptr) {
     const double dt = dot(r.d, oc);  // b / 2
-    if (dt > 0) return;
     const double x = dt * dt - r.a * c;  // det / 4
-    if (!(x >= 0)) return;
+    if (RT_SPHERE_ONEBRANCH) {
+        if (dt > 0 || !(x >= 0)) return;  // one branch for both rejections
+    } else {
+        if (dt > 0) return;
+        if (!(x >= 0)) return;
+    }
     DIAG(2);
     double proj, pt;
     if (x == 0) {
@@ -1283,12 +1293,14 @@ __device__ __forceinline__ void walls_f(const KParams& p, f3 o, f3 d, float& bes
         const f3 nw = F3(Wl.n[0], Wl.n[1], Wl.n[2]), P = F3(Wl.P[0], Wl.P[1], Wl.P[2]);
         const float den = fdot(nw, d);
         const float num = fdot(P - o, nw);
-        if (!((num > 0 && den > 0) || (num < 0 && den < 0))) continue;
+        // RT_F32_WALL_FLAT: no sign pre-test branch; t <= 0, NaN and inf fail below
+        if (!RT_F32_WALL_FLAT && !((num > 0 && den > 0) || (num < 0 && den < 0))) continue;
         const float t = num * frcp(den);
         const f3 q = fmad3(d, t, o) - P;
         const float px = fdot(q, F3(Wl.X[0], Wl.X[1], Wl.X[2]));
         const float py = fdot(q, F3(Wl.Y[0], Wl.Y[1], Wl.Y[2]));
-        if (t > 0 && px >= 0 && px <= Wl.len && py >= 0 && py <= Wl.wid) {
+        const bool sgn = RT_F32_WALL_FLAT || ((num > 0 && den > 0) || (num < 0 && den < 0));
+        if (sgn && t > 0 && px >= 0 && px <= Wl.len && py >= 0 && py <= Wl.wid) {
             bool take = t < best;
             if (!take && t == best && slot >= 0) take = p.wall_j[w] < scene_index(p, slot);
             if (take) {
