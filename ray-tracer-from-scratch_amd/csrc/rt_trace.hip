@@ -58,6 +58,9 @@
 #ifndef RT_F32_WALL_FLAT   // F32 wall test without the sign pre-test branch: one branch per wall
 #define RT_F32_WALL_FLAT 1
 #endif
+#ifndef RT_WALL_BOUNDS_FLAT  // A/B knob: the wall's four bounds in one predicate (measured
+#define RT_WALL_BOUNDS_FLAT 0    // neutral at c1-c5: off)
+#endif
 #ifndef RT_SPHERE_ONEBRANCH  // 1: Sphere::intersect's two early rejections (b > 0, det < 0)
 #define RT_SPHERE_ONEBRANCH 1  // share one branch (det/4 formed for every lane: 2 VALU)
 #endif
@@ -208,7 +211,27 @@ __device__ __forceinline__ double sqrt_fast(double x) {
     d = __builtin_fma(-g, g, x);
     return __builtin_fma(d, h, g);
 }
+#ifndef RT_SQRT_FLAT      // A/B knob (off: +2..4% VALU-bound): 1 = sqrt_e without a branch: LLVM's own range scaling (x < 2^-767 is
+#define RT_SQRT_FLAT 0    // scaled by 2^256, the root by 2^-128) and its +-0/+inf passthrough as
+#endif                    // selects — the same instructions the library path runs, so the same bits
 __device__ __forceinline__ double sqrt_e(double x) {
+    if (RT_SQRT_FLAT) {
+        const bool sm = x < 0x1p-767;
+        const double xs = __builtin_amdgcn_ldexp(x, sm ? 256 : 0);
+        const double y = __builtin_amdgcn_rsq(xs);
+        double g = xs * y;
+        double h = y * 0.5;
+        const double r = __builtin_fma(-h, g, 0.5);
+        g = __builtin_fma(g, r, g);
+        double d = __builtin_fma(-g, g, xs);
+        h = __builtin_fma(h, r, h);
+        g = __builtin_fma(d, h, g);
+        d = __builtin_fma(-g, g, xs);
+        g = __builtin_fma(d, h, g);
+        g = __builtin_amdgcn_ldexp(g, sm ? -128 : 0);
+        // +-0 and +inf are their own roots (LLVM: v_cmp_class mask 0x260)
+        return __builtin_amdgcn_class(xs, 0x260) ? xs : g;
+    }
     if (RT_SQRT_UNIFORM) {
         const bool ok = x >= 0x1p-767;
         if (__builtin_expect(__ballot(!ok) != 0, 0)) return ok ? sqrt_fast(x) : sqrt(x);
@@ -410,7 +433,11 @@ __device__ __forceinline__ void wall_exact(const Wall64& Wl, int w, const KParam
     const d3 q = (r.o + r.d * t) - P;  // ray::at (scene.h:16) minus the corner
     const double px = dot(q, ld3(Wl.X));
     const double py = dot(q, ld3(Wl.Y));
-    if (px >= 0 && px <= Wl.len && py >= 0 && py <= Wl.wid) {
+    // RT_WALL_BOUNDS_FLAT: all four bounds in one predicate (no branch between px and py)
+    const bool inb = RT_WALL_BOUNDS_FLAT
+                         ? ((px >= 0) & (px <= Wl.len) & (py >= 0) & (py <= Wl.wid))
+                         : (px >= 0 && px <= Wl.len && py >= 0 && py <= Wl.wid);
+    if (inb) {
         bool take = t < h.dist;
         if (!take && t == h.dist && h.slot >= 0)  // tie: the lower scene index wins (rare)
             take = p.wall_j[w] < scene_index(p, h.slot);
@@ -1766,6 +1793,16 @@ __global__ void k_selftest(int which, uint64_t n, uint64_t seed, unsigned long l
             if (__double_as_longlong(sqrt_e(a)) != __double_as_longlong(sqrt(a))) ++nbad;
             const double b = (double)(z1 >> 11) * (1.0 / 9007199254740992.0);  // [0,1)
             if (__double_as_longlong(sqrt_e(b)) != __double_as_longlong(sqrt(b))) ++nbad;
+            // the scaled range: subnormals and tiny normals up to 2^-700, and 0 / inf
+            const uint64_t z2 = mix64(seed + 3 * i + 2);
+            const uint64_t ex = z2 % 324;  // biased exponent 0 (subnormal) .. 323
+            const double c = __longlong_as_double((long long)((ex << 52) | (z1 & 0xFFFFFFFFFFFFFull)));
+            if (__double_as_longlong(sqrt_e(c)) != __double_as_longlong(sqrt(c))) ++nbad;
+            if (i == 0) {
+                const double sp[3] = {0.0, -0.0, __builtin_inf()};
+                for (int k = 0; k < 3; ++k)
+                    if (__double_as_longlong(sqrt_e(sp[k])) != __double_as_longlong(sqrt(sp[k]))) ++nbad;
+            }
         } else {
             const double x = (double)(z0 >> 11) * (1.0 / 9007199254740992.0);  // [0,1)
             const double e = (double)(1 + (z1 % 64));
