@@ -140,7 +140,9 @@ int rt_capi_version(void);
 
 /* ---- scene -------------------------------------------------------------- */
 /* Copies n primitives (in scene order: index j is the reference's scene.at(j)) to the
- * device.  Replaces any previous scene.  n == 0 is a valid (empty) scene. */
+ * device.  Replaces any previous scene.  n == 0 is a valid (empty) scene.  Waits first
+ * for every render this ctx has enqueued, on its own stream and on caller streams
+ * (rt_render_device), so frames in flight finish on the old scene. */
 int rt_set_scene(rt_ctx* ctx, const rt_prim* prims, int32_t n);
 
 /* ---- tuning ------------------------------------------------------------- */
@@ -197,7 +199,10 @@ int rt_render(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nrows, in
 /* Same, but `d_out` is DEVICE memory and the launch is enqueued on `stream`
  * (a hipStream_t; NULL = the ctx's stream) without synchronising: the hot path as a
  * bench or a multi-GPU tiler drives it.  If d_segments != NULL it must point to one
- * device uint64 that receives += the segment count. */
+ * device uint64 that receives += the segment count.  The launch signals a per-stream
+ * event of the ctx that rt_set_scene / rt_ctx_destroy wait on (up to 16 streams are
+ * tracked; a 17th retires the oldest by waiting on it).  Every entry point runs on the
+ * ctx's device and leaves the caller's current device unchanged. */
 int rt_render_device(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nrows,
                      int32_t depth, int32_t precision, uint32_t flags, int32_t out_format,
                      void* d_out, uint64_t* d_segments, void* stream);
