@@ -73,6 +73,9 @@
 #ifndef RT_LAZY_TERMS      // PATH64: |d|^2, 1/|d|^2, |d| only when a sphere test or a
 #define RT_LAZY_TERMS 0    // reflection needs them (wave-uniform; A/B: +2% at c2, off)
 #endif
+#ifndef RT_PEEL            // 1: the primary segment peeled off the bounce loop (straight-line)
+#define RT_PEEL 1
+#endif
 #ifndef RT_SKY_FAST        // PATH64/F32 linear scan: a tile whose keep mask is empty (no primitive's
 #define RT_SKY_FAST 1      // pixel box meets it: every primary ray misses) shades its sky/ground
 #endif                     // at once, without |d|^2, 1/|d|^2, |d| or the bounce loop
@@ -233,11 +236,13 @@ __device__ __forceinline__ double sqrt_e(double x) {
         return __builtin_amdgcn_class(xs, 0x260) ? xs : g;
     }
     if (RT_SQRT_UNIFORM) {
-        const bool ok = x >= 0x1p-767;
+        const bool ok = x >= 0x1p-767 && x <= DBL_MAX;
         if (__builtin_expect(__ballot(!ok) != 0, 0)) return ok ? sqrt_fast(x) : sqrt(x);
         return sqrt_fast(x);
     }
-    if (!(x >= 0x1p-767)) return sqrt(x);
+    // tiny, zero, negative, NaN and +inf take the library path (+inf: rsq(inf) = 0 would
+    // give inf * 0 = NaN below; the library passes inf through)
+    if (!(x >= 0x1p-767 && x <= DBL_MAX)) return sqrt(x);
     const double y = __builtin_amdgcn_rsq(x);
     double g = x * y;
     double h = y * 0.5;
@@ -1116,14 +1121,10 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
     int n = 0;
     d3 c64 = D3(0, 0, 0);
     f3 c32 = F3(0.f, 0.f, 0.f);
-    // Converged bounce loop: lanes whose path ended stay (alive == false) so the wave can
-    // reduce over its live rays; k is wave-uniform.
-    int kend = 0;  // wave-uniform: bounce iterations run (every lane's n <= kend)
-    for (int k = 0;; ++k) {
-        if (!__any(alive)) {
-            kend = k;
-            break;
-        }
+    // One segment (one closest-hit query per live lane) at bounce k.  Converged: lanes
+    // whose path ended stay (alive == false) so the wave can reduce over its live rays; k
+    // is wave-uniform.
+    auto segment = [&](const int k) __attribute__((always_inline)) {
         bounce_priority(k);
         // tile bins: the primary segment, and the first bounce when the whole wave
         // reflected off one wall (both wave-uniform)
@@ -1147,7 +1148,7 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
             ray_terms(r);
             terms = true;
         }
-        if (!alive) continue;
+        if (!alive) return;
         ++segs;
         if (!COLOR64 && RT_TERMINAL_F32 && (last || h.slot < 0)) {
             // PATH64, last segment of the path: nothing here feeds another ray
@@ -1169,7 +1170,7 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
                 c32 = local_color_f(m32, sh.x, sh.y, sun);
             }
             alive = false;
-            continue;
+            return;
         }
         DIAG(8);
         const double rdl = rcp_refined(r.dlen);
@@ -1185,7 +1186,7 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
                          fmaf(tz, 0.49f - 0.57f, 0.57f));
             }
             alive = false;
-            continue;
+            return;
         }
         const d3 pos = r.o + r.d * h.dist;  // main.cpp:99 (sphere world distance used as t)
         d3 N;
@@ -1216,7 +1217,7 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
             else
                 c32 = local_color_f(p.mat32[h.slot], s, ks, sun);
             alive = false;
-            continue;
+            return;
         }
         st_s[k] = s;
         st_k[k] = ks;
@@ -1229,6 +1230,30 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
             terms = false;
         } else {
             r = make_ray(pos + N * .0001, nv - nn * cc);
+        }
+        };
+    // The primary segment is peeled off the bounce loop (RT_PEEL): it runs as straight-line
+    // code with k == 0 folded, so the loop's phi copies and control are only paid by waves
+    // that bounce.
+    int kend = 0;  // wave-uniform: bounce iterations run (every lane's n <= kend)
+    if (RT_PEEL) {
+        if (__any(alive)) {
+            segment(0);
+            for (int k = 1;; ++k) {
+                if (!__any(alive)) {
+                    kend = k;
+                    break;
+                }
+                segment(k);
+            }
+        }
+    } else {
+        for (int k = 0;; ++k) {
+            if (!__any(alive)) {
+                kend = k;
+                break;
+            }
+            segment(k);
         }
     }
     STAGE(3);
