@@ -73,8 +73,8 @@
 #ifndef RT_LAZY_TERMS      // PATH64: |d|^2, 1/|d|^2, |d| only when a sphere test or a
 #define RT_LAZY_TERMS 0    // reflection needs them (wave-uniform; A/B: +2% at c2, off)
 #endif
-#ifndef RT_PEEL            // 1: the primary segment peeled off the bounce loop (straight-line)
-#define RT_PEEL 1
+#ifndef RT_PEEL            // 1: the primary segment peeled off the bounce loop (straight-line);
+#define RT_PEEL 2          // 2: the first bounce too (c2 PATH64 -3%, F64 -4% over 1)
 #endif
 #ifndef RT_SKY_FAST        // PATH64/F32 linear scan: a tile whose keep mask is empty (no primitive's
 #define RT_SKY_FAST 1      // pixel box meets it: every primary ray misses) shades its sky/ground
@@ -1236,7 +1236,23 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
     // code with k == 0 folded, so the loop's phi copies and control are only paid by waves
     // that bounce.
     int kend = 0;  // wave-uniform: bounce iterations run (every lane's n <= kend)
-    if (RT_PEEL) {
+    if (RT_PEEL >= 2) {
+        if (__any(alive)) {
+            segment(0);
+            if (!__any(alive)) {
+                kend = 1;
+            } else {
+                segment(1);
+                for (int k = 2;; ++k) {
+                    if (!__any(alive)) {
+                        kend = k;
+                        break;
+                    }
+                    segment(k);
+                }
+            }
+        }
+    } else if (RT_PEEL) {
         if (__any(alive)) {
             segment(0);
             for (int k = 1;; ++k) {
@@ -1402,12 +1418,7 @@ __device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, bool
         }
         return c;
     }
-    int kend = 0;  // wave-uniform: bounce iterations run (every lane's n <= kend)
-    for (int k = 0;; ++k) {
-        if (!__any(alive)) {
-            kend = k;
-            break;
-        }
+    auto segment = [&](const int k) __attribute__((always_inline)) {
         bounce_priority(k);
         const float a = fdot(d, d);
         const float ra = frcp(a);
@@ -1476,7 +1487,7 @@ __device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, bool
                 }
             }
         }
-        if (!alive) continue;
+        if (!alive) return;
         ++segs;
         if (!CULL && !binned) walls_f(p, o, d, best, slot);
         const f3 nv = d * rl;
@@ -1489,7 +1500,7 @@ __device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, bool
                        fmaf(tz, 0.49f - 0.57f, 0.57f));
             }
             alive = false;
-            continue;
+            return;
         }
         const f3 pos = fmad3(d, best, o);
         f3 N;
@@ -1506,7 +1517,7 @@ __device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, bool
         if (k >= p.depth || k >= MAXD) {
             c = local_color_f(m, sh.x, sh.y, sun);
             alive = false;
-            continue;
+            return;
         }
         st_s[k] = sh.x;
         st_k[k] = sh.y;
@@ -1515,6 +1526,45 @@ __device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, bool
         const float cc = 2.0f * fdot(nv, nn);
         o = fmad3(N, 1e-4f, pos);
         d = fmad3(nn, -cc, nv);
+        };
+    int kend = 0;  // wave-uniform: bounce iterations run (every lane's n <= kend)
+    // the primary segment and the first bounce peeled (see trace_pixel_d); the F32 cull
+    // kernels peel the primary only (the second copy: c3 +6%, c5 +9%)
+    if (RT_PEEL >= 2 && !CULL) {
+        if (__any(alive)) {
+            segment(0);
+            if (!__any(alive)) {
+                kend = 1;
+            } else {
+                segment(1);
+                for (int k = 2;; ++k) {
+                    if (!__any(alive)) {
+                        kend = k;
+                        break;
+                    }
+                    segment(k);
+                }
+            }
+        }
+    } else if (RT_PEEL) {
+        if (__any(alive)) {
+            segment(0);
+            for (int k = 1;; ++k) {
+                if (!__any(alive)) {
+                    kend = k;
+                    break;
+                }
+                segment(k);
+            }
+        }
+    } else {
+        for (int k = 0;; ++k) {
+            if (!__any(alive)) {
+                kend = k;
+                break;
+            }
+            segment(k);
+        }
     }
     for (int q = MAXD - 1; q >= 0; --q) {
         if ((!RT_UNWIND_KEND || q < kend) && q < n) {  // uniform test: levels no lane reached
