@@ -17,6 +17,22 @@
 
 #include "../../include/rt_capi.h"
 #include "rt_device.h"
+#include <chrono>
+
+#ifndef RT_HOST_PROFILE   // diagnostic build: per-phase host time of rt_render_device, printed
+#define RT_HOST_PROFILE 0 // to stderr by rt_ctx_destroy (never in the product)
+#endif
+#if RT_HOST_PROFILE
+static double g_hp[5];
+static long g_hn;
+static inline double hp_now() {
+    return std::chrono::duration<double, std::micro>(
+               std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+#define HP(i) (g_hp[(i)] += (g_hn > 50 ? hp_now() - hp_t : 0.0), hp_t = hp_now())  // warm calls only
+#else
+#define HP(i) ((void)0)
+#endif
 
 struct rt_ctx {
     int device = 0;
@@ -814,6 +830,13 @@ int rt_ctx_create(int device, rt_ctx** out) {
 
 int rt_ctx_destroy(rt_ctx* ctx) {
     if (!ctx) return RT_ERR_INVALID_ARG;
+#if RT_HOST_PROFILE
+    if (g_hn > 50) {
+        const double m = (double)(g_hn - 50);
+        std::fprintf(stderr, "host profile over %ld warm renders (us): args %.2f params %.2f rows+event %.2f launch %.2f snapshot %.2f\n",
+                     g_hn - 50, g_hp[0] / m, g_hp[1] / m, g_hp[2] / m, g_hp[3] / m, g_hp[4] / m);
+    }
+#endif
     DeviceGuard dg(ctx->device);
     (void)wait_inflight(ctx);  // frames in flight on caller streams still read the scene
     for (auto& f : ctx->inflight) (void)hipEventDestroy(f.ev);
@@ -1055,6 +1078,10 @@ static int snapshot_costs(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32
 int rt_render_device(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nrows,
                      int32_t depth, int32_t precision, uint32_t flags, int32_t out_format,
                      void* d_out, uint64_t* d_segments, void* stream) {
+#if RT_HOST_PROFILE
+    double hp_t = hp_now();
+    g_hn++;
+#endif
     int st = check_render_args(ctx, cam, row0, nrows, depth, precision, out_format);
     if (st != RT_OK) return st;
     if (!d_out && nrows > 0 && cam->width > 0) return RT_ERR_INVALID_ARG;
@@ -1062,8 +1089,10 @@ int rt_render_device(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nr
     // device the caller has current
     DeviceGuard dg(ctx->device);
     RT_HIP(ctx, dg.err);
+    HP(0);
     rt::KParams p = make_params(ctx, cam, row0, nrows, depth, flags, out_format, d_out,
                                 reinterpret_cast<unsigned long long*>(d_segments));
+    HP(1);
     void* s = stream ? stream : static_cast<void*>(ctx->stream);
     hipStream_t hs = static_cast<hipStream_t>(s);
     st = prepare_rows(ctx, cam, row0, nrows, hs, p);
@@ -1071,9 +1100,13 @@ int rt_render_device(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nr
     hipEvent_t done = nullptr;
     st = launch_event(ctx, hs, &done);
     if (st != RT_OK) return st;
+    HP(2);
     const int e = rt::launch_trace(p, precision, s, done);
     if (e != (int)hipSuccess) return hip_fail(ctx, (hipError_t)e, "launch k_trace");
-    return snapshot_costs(ctx, cam, row0, nrows, hs, p);
+    HP(3);
+    st = snapshot_costs(ctx, cam, row0, nrows, hs, p);
+    HP(4);
+    return st;
 }
 
 int rt_render(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nrows, int32_t depth,
