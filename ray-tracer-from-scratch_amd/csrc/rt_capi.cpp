@@ -285,6 +285,9 @@ struct BoxAcc {
     }
 };
 
+#ifndef RT_SPHERE_BOX_INTERVAL  // 1: sphere pixel boxes from the exact extent of the ball (two
+#define RT_SPHERE_BOX_INTERVAL 1  // quadratics); 0: from the 8 corners of its bounding cube
+#endif
 /* Boxes of every primitive (material-slot order) for the camera P (origin P.o). */
 void boxes_for(const rt_ctx* ctx, const Proj& P, double dmax, int32_t width, int32_t row0,
                int32_t nrows, rt::PrimBox* out) {
@@ -301,6 +304,17 @@ void boxes_for(const rt_ctx* ctx, const Proj& P, double dmax, int32_t width, int
     };
     const double* o = P.o;
     const double oabs = std::fabs(o[0]) + std::fabs(o[1]) + std::fabs(o[2]);
+#if RT_SPHERE_BOX_INTERVAL
+    // Exact x (and i) extent of the ball: the pixels with p/u = x form the plane
+    // (b - x a).(X - o) = 0 through o (a, b, c = rows of M^-1), and it meets the ball
+    // |X - C| <= r iff |(b - x a).(C - o)| <= r |b - x a|, i.e. x lies between the roots of
+    // (uc^2 - r^2 |a|^2) x^2 - 2 (pc uc - r^2 a.b) x + (pc^2 - r^2 |b|^2) = 0 (the ball wholly
+    // in front, u0 > 0, makes the leading coefficient positive).  Rounding is covered by the
+    // one-pixel widening of to_box, as for the other hulls.
+    const double aa = dot3(P.r[0], P.r[0]), ab = dot3(P.r[0], P.r[1]), ac = dot3(P.r[0], P.r[2]),
+                 bb = dot3(P.r[1], P.r[1]), cc = dot3(P.r[2], P.r[2]);
+    const double na = std::sqrt(aa);
+#endif
     for (int s = 0; s < ctx->sc.nS; s++) {
         const double* S = &ctx->sc.h_sph[5 * s];
         const double r = S[4];
@@ -308,6 +322,28 @@ void boxes_for(const rt_ctx* ctx, const Proj& P, double dmax, int32_t width, int
         const double delta = 1e-6 * (1 + oabs + std::fabs(S[0]) + std::fabs(S[1]) + std::fabs(S[2]) + r);
         rt::PrimBox b = all;
         if (std::sqrt(dot3(v, v)) > r * 1.7320508075688772 + delta && r > 1e-9 * std::sqrt(dot3(v, v))) {
+#if RT_SPHERE_BOX_INTERVAL
+            const double uc = dot3(P.r[0], v), pc = dot3(P.r[1], v), qc = dot3(P.r[2], v);
+            const double u0 = uc - r * na, u1 = uc + r * na;
+            if (u1 < 0) {
+                b = none;
+            } else if (u0 > 0) {
+                const double r2 = r * r;
+                const double A = uc * uc - r2 * aa;
+                const double Bx = pc * uc - r2 * ab, Cx = pc * pc - r2 * bb;
+                const double By = qc * uc - r2 * ac, Cy = qc * qc - r2 * cc;
+                const double sx = std::sqrt(std::fmax(0.0, Bx * Bx - A * Cx));
+                const double sy = std::sqrt(std::fmax(0.0, By * By - A * Cy));
+                BoxAcc acc;
+                acc.x0 = (Bx - sx) / A;
+                acc.x1 = (Bx + sx) / A;
+                acc.i0 = (By - sy) / A;
+                acc.i1 = (By + sy) / A;
+                acc.bad = !(A > 0) || !std::isfinite(acc.x0) || !std::isfinite(acc.x1) ||
+                          !std::isfinite(acc.i0) || !std::isfinite(acc.i1);
+                b = to_box(acc);
+            }
+#else
             double umin = INFINITY, umax = -INFINITY;
             double X[8][3];
             for (int c = 0; c < 8; c++) {
@@ -323,6 +359,7 @@ void boxes_for(const rt_ctx* ctx, const Proj& P, double dmax, int32_t width, int
                 for (int c = 0; c < 8; c++) acc.add(P, X[c]);
                 b = to_box(acc);
             }
+#endif
         }
         out[s] = b;
     }
