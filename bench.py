@@ -7,7 +7,11 @@ renders one full frame of the configured scene (default c2: 1920x1080, 8 spheres
 already resident on the device.  With N ranks the batch is N frames of a camera
 fly-through (rank r renders frame r: the camera moved r steps forward the way
 Camera::forward moves it, scene.cpp:121) — frames are independent units, sharded with
-no data-path collective, so `scaling` is "weak".  `--mode tiled` instead splits ONE
+no data-path collective, so `scaling` is "weak".  Consecutive frames of a rank go to
+`--frames-in-flight` output buffers on as many streams (default 3, a triple-buffered frame
+loop): every frame is rendered in full, and one frame's last (heaviest) waves overlap the
+next frame's first instead of leaving the GPU draining between launches; `kernel_ms` is
+the one-frame-at-a-time kernel duration.  `--mode tiled` instead splits ONE
 frame into row bands across ranks and gathers them to rank 0 (RCCL), the strong-scaling
 layout of BASELINE config 4.
 
@@ -105,6 +109,10 @@ def main() -> int:
     ap.add_argument("--out", default="rgb_f32", choices=["rgb_f32", "rgba8"],
                     help="timed output format: linear fp32 RGB (12 B/px, parity buffer) or the "
                          "clamp+truncate RGBA8 epilogue (4 B/px; cuts the tiled gather 3x)")
+    ap.add_argument("--frames-in-flight", type=int, default=3,
+                    help="frames mode: consecutive frames go to F output buffers on F streams "
+                         "(a triple-buffered frame loop), so one frame's last waves overlap the "
+                         "next frame's first; 1 = one stream, frames back to back")
     ap.add_argument("--sun", action="store_true", help="build-defined sun term (off = parity)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -159,19 +167,23 @@ def main() -> int:
         row0, nrows = capi.band_rows(H, world, rank)
     band_max = -(-H // world) if args.mode == "tiled" else H
 
-    # a dedicated stream: the C-ABI maps a NULL stream to its own, so torch's legacy
+    # dedicated streams: the C-ABI maps a NULL stream to its own, so torch's legacy
     # default stream (handle 0) would put the launches and the timing events apart
-    stream = torch.cuda.Stream(dev)
+    fif = max(1, args.frames_in_flight) if args.mode == "frames" else 1
+    streams = [torch.cuda.Stream(dev) for _ in range(fif)]
+    stream = streams[0]
     torch.cuda.set_stream(stream)
-    # sized for fp32 RGB: the per-precision sweep below always writes 12 B/px into it
-    out = torch.empty((band_max, W, 3), dtype=torch.float32, device=dev)
+    # sized for fp32 RGB: the per-precision sweep below always writes 12 B/px into them;
+    # frames in flight: one output buffer per stream (every frame is rendered in full)
+    outs = [torch.empty((band_max, W, 3), dtype=torch.float32, device=dev) for _ in range(fif)]
+    out = outs[0]
     out_fmt = capi.RT_OUT_RGBA8 if args.out == "rgba8" else capi.RT_OUT_RGB_F32
     segs_t = torch.zeros(1, dtype=torch.int64, device=dev)
 
-    def launch(d_segs: int = 0, dst=None):
-        rend.render_device(cam, depth, (dst if dst is not None else out).data_ptr(), prec, flags,
-                           out_fmt, row0=row0, nrows=nrows, d_segments=d_segs,
-                           stream=stream.cuda_stream)
+    def launch(d_segs: int = 0, dst=None, slot: int = 0):
+        rend.render_device(cam, depth, (dst if dst is not None else outs[slot]).data_ptr(), prec,
+                           flags, out_fmt, row0=row0, nrows=nrows, d_segments=d_segs,
+                           stream=streams[slot].cuda_stream)
 
     tiled = None
     if args.mode == "tiled" and world > 1:
@@ -182,11 +194,20 @@ def main() -> int:
                                    torch.uint8 if args.out == "rgba8" else torch.float32,
                                    dev, depth=2)
 
+    nstep = [0]
+
     def step():
         if tiled is not None:
             tiled.submit()
         else:
-            launch()
+            launch(slot=nstep[0] % fif)
+            nstep[0] += 1
+
+    def join_streams():
+        # stream 0 waits for every other stream's work (the end-of-region event is then
+        # behind every frame of the region)
+        for s_ in streams[1:]:
+            stream.wait_stream(s_)
 
     # census: exact segment count of this rank's share (untimed)
     launch(segs_t.data_ptr())
@@ -211,6 +232,7 @@ def main() -> int:
         step()
     if tiled is not None:
         tiled.drain()
+    join_streams()
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     barrier()
@@ -221,7 +243,7 @@ def main() -> int:
     elapsed_s = float(elapsed.item())
     stream_ms = ev0.elapsed_time(ev1) / args.steps
 
-    # per-launch kernel time (HIP events around launches alone, same stream)
+    # per-launch kernel time: one stream, launches back to back (HIP events on that stream)
     ek0 = torch.cuda.Event(enable_timing=True)
     ek1 = torch.cuda.Event(enable_timing=True)
     nk = max(10, args.steps)
@@ -345,9 +367,12 @@ def main() -> int:
                                 else f"row-tiled x{world} + gather"),
                 "host_box_cache": bool(args.box_cache),
                 "row_feedback": args.row_feedback,
+                "frames_in_flight": fif,
             },
             "ms_per_frame": round(ms_step / frames_per_step if args.mode == "frames" else ms_step, 4),
             "mpx_per_s": round(px_step * args.steps / elapsed_s / 1e6, 2),
+            # one frame at a time on one stream (HIP events around back-to-back launches):
+            # the per-frame latency, and the kernel duration the rooflines are priced on
             "kernel_ms": round(kernel_ms, 4),
             "stream_ms_per_step": round(stream_ms, 4),
             "roofline": {
