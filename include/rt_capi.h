@@ -172,12 +172,15 @@ enum rt_option {
                                          options equal the previous render's reuses its
                                          per-frame pixel boxes (host work only); 0 = always
                                          recompute.  Output is identical. */
-    RT_OPT_ROW_FEEDBACK = 8           /* N > 0 (default 32): every render records each
+    RT_OPT_ROW_FEEDBACK = 8,          /* N > 0 (default 32): every render records each
                                          tile's cost; every N frames (and at once for a new
                                          band or scene) a snapshot is copied back behind the
                                          kernel, and later renders of the same band dispatch
                                          tile rows heaviest-first by it (scheduling only);
                                          0 = off.  Output is identical. */
+    RT_OPT_PIXEL_PAIRS = 9            /* 1: RT_PREC_PATH64 renders without the wave cull
+                                         trace two pixels per lane (16x8 pixels per
+                                         wave); 0 (default) = one.  Output is identical. */
 };
 int rt_set_option(rt_ctx* ctx, int32_t option, int64_t value);
 

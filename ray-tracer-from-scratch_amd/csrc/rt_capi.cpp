@@ -5,6 +5,9 @@
  * timing events and a staging buffer for host-output renders.  No exception crosses
  * the boundary; every entry point returns an rt_status.
  */
+#ifndef RT_PIXEL_PAIRS_DEFAULT  // build-time default of RT_OPT_PIXEL_PAIRS (A/B builds)
+#define RT_PIXEL_PAIRS_DEFAULT 0
+#endif
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -64,6 +67,7 @@ struct rt_ctx {
     // most expensive tile (heaviest first) for the following renders of the same band.
     // Only the dispatch order changes: every tile is traced once per frame either way.
     int feedback = 32;             // refresh interval in frames, 0 = off
+    bool pixel_pairs = RT_PIXEL_PAIRS_DEFAULT;  // RT_OPT_PIXEL_PAIRS
     uint16_t* d_cost = nullptr;    // device, d_cost_cap entries
     uint16_t* h_cost = nullptr;    // pinned host snapshot
     size_t d_cost_cap = 0;
@@ -558,6 +562,7 @@ rt::KParams make_params(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, i
     }
     p.out = d_out;
     p.segs = d_segs;
+    p.pairs = ctx->pixel_pairs ? 1 : 0;
     p.stats = ctx->d_stats;
     // eye tables (rt_device.h) for the linear-scan kernels: the same fp64 operations, in
     // the same order, as sphere_exact / wall_exact on a ray starting at cam->position
@@ -971,6 +976,10 @@ int rt_set_option(rt_ctx* ctx, int32_t option, int64_t value) {
         case RT_OPT_ROW_ORDER:
             if (value != 0 && value != 1) return RT_ERR_INVALID_ARG;
             ctx->row_order = value == 1;
+            return RT_OK;
+        case RT_OPT_PIXEL_PAIRS:
+            if (value != 0 && value != 1) return RT_ERR_INVALID_ARG;
+            ctx->pixel_pairs = value == 1;
             return RT_OK;
         case RT_OPT_ROW_FEEDBACK:
             if (value < 0 || value > 1000000) return RT_ERR_INVALID_ARG;

@@ -152,7 +152,8 @@ struct KParams {
     int16_t row_perm[ROW_PERM_MAX];  // dispatch order of tile rows (rt_trace.hip tile_row)
     PrimBox box[BIN_MAX_PRIMS]; // material-slot order: spheres, then walls
     int32_t mir_depth;          // wall-sequence levels with mirror boxes (0 = off)
-    int32_t pad_mir;
+    int32_t pairs;              // RT_OPT_PIXEL_PAIRS: PATH64 linear-scan frames trace two
+                                // pixels per lane (16x8 pixels per wave)
     PrimBox mbox[MIR_MAX_BOXES];  // [sequence][slot j]: primitive j through the camera
                                   // mirrored along the sequence (see above)
     int32_t eye;                        // eye tables below valid

@@ -1294,6 +1294,310 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
 }
 
 /* ------------------------------------------------------------------------ */
+/* PATH64, two pixels per lane (RT_OPT_PIXEL_PAIRS)                          */
+/* ------------------------------------------------------------------------ */
+/* A wave traces a 16x8 tile: lane l holds pixel (x0 + l%8, i0 + l/8) and the pixel 8
+ * columns to its right.  At c2 the primary pass issues about as many SALU, branch and
+ * scalar-load instructions as VALU and a SIMD issues ~one instruction per
+ * quad-cycle there; those are per-wave costs (the primitive's record, the loop, the
+ * exec-mask bookkeeping of each test's branch), so two pixels per lane pay them once for
+ * 128 pixels, and each test's two independent dependency chains share one branch.
+ * Every test is trace_pixel_d's (PATH64: exact fp64 paths, fp32 colour) evaluated for
+ * both pixels of the lane under ONE branch taken when either pixel needs its body; the
+ * results are kept by predicated selects, so each pixel's hit, path and colour are
+ * bitwise those of the one-pixel kernel (tested: test_pixel_pairs_bitwise). */
+template <int MAXD>
+struct PxS {  // one pixel's path state (its register stack lives in separate arrays: the
+    RayD r;   // promotion of a dynamically indexed array to registers needs an array alloca)
+    int n;
+    f3 c;
+    bool alive;
+};
+
+
+/* sphere_exact_oc's accept path for one pixel, branch-free given g (the early rejections
+ * passed).  The x == 0 case of scene.cpp:64-66 folds in: sqrt(0) = 0 gives num == -dt
+ * exactly, so q = div_r(num, a) is its pt and its proj is 2q (the reference's /a); for
+ * x > 0 num <= 0 gives q <= 0, rejected by dist > 0 as sphere_exact_oc's num test does. */
+__device__ __forceinline__ void sphere_accept(double dt, double x, bool g, int s, const RayD& r,
+                                              HitD& h) {
+    const bool x0 = x == 0;
+    const double sq = sqrt_e(g && !x0 ? x : 1.0);
+    const double num = -dt - (x0 ? 0.0 : sq);
+    const double q = div_r(num, r.a, r.ra);
+    const double dist = (x0 ? 2.0 * q : q) * r.dlen;  // world distance, scene.cpp:77
+    const bool take = g && num > 0 && dist > 0 && dist < h.dist;
+    h.dist = take ? dist : h.dist;
+    h.pt = take ? q : h.pt;
+    h.slot = take ? s : h.slot;
+}
+/* Sphere s for both pixels (spheres in index order: strict < keeps the earlier). */
+template <int MAXD>
+__device__ __forceinline__ void sphere_pair(const d3 oc0, double c0, const d3 oc1, double c1,
+                                            int s, const PxS<MAXD>& a, const PxS<MAXD>& b,
+                                            HitD& ha, HitD& hb) {
+    const double dta = dot(a.r.d, oc0), dtb = dot(b.r.d, oc1);
+    const double xa = dta * dta - a.r.a * c0, xb = dtb * dtb - b.r.a * c1;
+    const bool ga = a.alive && !(dta > 0 || !(xa >= 0));
+    const bool gb = b.alive && !(dtb > 0 || !(xb >= 0));
+    if (ga || gb) {
+        DIAG(2);
+        sphere_accept(dta, xa, ga, s, a.r, ha);
+        sphere_accept(dtb, xb, gb, s, b.r, hb);
+    }
+}
+/* wall_exact's bounds test and take for one pixel, branch-free given g (t > 0, t <= best). */
+__device__ __forceinline__ void wall_accept(const Wall64& Wl, int w, const KParams& p, double t,
+                                            bool g, const RayD& r, const d3 P, HitD& h) {
+    const d3 q = (r.o + r.d * t) - P;  // ray::at (scene.h:16) minus the corner
+    const double px = dot(q, ld3(Wl.X));
+    const double py = dot(q, ld3(Wl.Y));
+    const bool inb = g && px >= 0 && px <= Wl.len && py >= 0 && py <= Wl.wid;
+    bool take = inb && t < h.dist;
+    if (inb && !take && t == h.dist && h.slot >= 0)  // tie: the lower scene index wins (rare)
+        take = p.wall_j[w] < scene_index(p, h.slot);
+    h.dist = take ? t : h.dist;
+    h.slot = take ? p.nS + w : h.slot;
+}
+template <bool EYE, int MAXD>
+__device__ __forceinline__ void wall_pair_px(const Wall64& Wl, int w, const KParams& p,
+                                             const PxS<MAXD>& a, const PxS<MAXD>& b, HitD& ha,
+                                             HitD& hb) {
+    const d3 n = ld3(Wl.n);
+    const d3 P = ld3(Wl.P);
+    const double dena = dot(n, a.r.d), denb = dot(n, b.r.d);
+    const double numa = EYE ? p.eye_w[w] : dot(P - a.r.o, n);
+    const double numb = EYE ? p.eye_w[w] : dot(P - b.r.o, n);
+    // as wall_exact (RT_WALL_NOSIGN, RT_WALL_TSKIP): t <= 0, NaN, +-inf and t > best fail
+    const double ta = div_r_nz(numa, dena, rcp_refined(dena));
+    const double tb = div_r_nz(numb, denb, rcp_refined(denb));
+    const bool ga = a.alive && ta > 0 && !(ta > ha.dist);
+    const bool gb = b.alive && tb > 0 && !(tb > hb.dist);
+    if (ga || gb) {
+        DIAG(6);
+        wall_accept(Wl, w, p, ta, ga, a.r, P, ha);
+        wall_accept(Wl, w, p, tb, gb, b.r, P, hb);
+    }
+}
+template <bool EYE, int MAXD>
+__device__ __forceinline__ void sphere_pair_idx(const KParams& p, int s, const PxS<MAXD>& a,
+                                                const PxS<MAXD>& b, HitD& ha, HitD& hb) {
+    if (EYE) {
+        const double* E = p.eye_s[s];
+        const d3 oc = D3(E[0], E[1], E[2]);
+        sphere_pair(oc, E[3], oc, E[3], s, a, b, ha, hb);
+    } else {
+        const double* S = p.s64[s >> 2].v[s & 3];
+        const d3 C = D3(S[0], S[1], S[2]);
+        const d3 oca = a.r.o - C, ocb = b.r.o - C;
+        sphere_pair(oca, lensq(oca) - S[3], ocb, lensq(ocb) - S[3], s, a, b, ha, hb);
+    }
+}
+/* closest_hit_bin / closest_hit_d for both pixels of every lane (keep wave-uniform). */
+template <bool EYE, int MAXD>
+__device__ __forceinline__ void scan_pair_bin(const KParams& p, const PxS<MAXD>& a,
+                                              const PxS<MAXD>& b, uint64_t keep, HitD& ha,
+                                              HitD& hb) {
+    uint64_t sm = p.nS >= 64 ? keep : keep & ((1ull << p.nS) - 1);
+    while (sm) {
+        const int s = __builtin_ctzll(sm);
+        sm &= sm - 1;
+        sphere_pair_idx<EYE>(p, s, a, b, ha, hb);
+    }
+    uint64_t wm = p.nS >= 64 ? 0 : keep >> p.nS;
+    while (wm) {
+        const int w = __builtin_ctzll(wm);
+        wm &= wm - 1;
+        wall_pair_px<EYE>(p.w64[w], w, p, a, b, ha, hb);
+    }
+}
+template <bool EYE, int MAXD>
+__device__ __forceinline__ void scan_pair_all(const KParams& p, const PxS<MAXD>& a,
+                                              const PxS<MAXD>& b, HitD& ha, HitD& hb) {
+    for (int s = 0; s < p.nS; ++s) sphere_pair_idx<EYE>(p, s, a, b, ha, hb);
+    for (int w = 0; w < p.nW; ++w) wall_pair_px<EYE>(p.w64[w], w, p, a, b, ha, hb);
+}
+
+/* Tile bins for a 16-pixel-wide tile (box_keep's compare, one ballot). */
+__device__ __forceinline__ uint64_t box_keep16(uint64_t raw, TileO t) {
+    const int x0 = (int16_t)(raw & 0xffff), x1 = (int16_t)((raw >> 16) & 0xffff);
+    const int i0 = (int16_t)((raw >> 32) & 0xffff), i1 = (int16_t)(raw >> 48);
+    const bool hit = (x0 <= t.x0 + 15) & (x1 >= t.x0) & (i0 <= t.y0 + 7) & (i1 >= t.y0);
+    return uniform64(__ballot(hit));
+}
+/* mirror_keep (RT_MIR_CHAINS = 1) over both pixels of every lane: the keep mask of the wall
+ * chain that every live pixel of the wave followed, or ~0. */
+template <int MAXD>
+__device__ __forceinline__ uint64_t mirror_keep_pair(const KParams& p, const PxS<MAXD>& a,
+                                                     const PxS<MAXD>& b, const int* ma,
+                                                     const int* mb, int k, TileO t) {
+    const uint64_t todo = uniform64(__ballot(a.alive || b.alive));
+    if (todo == 0 || k > p.mir_depth) return ~0ull;
+    const int l0 = __builtin_ctzll(todo);
+    const bool lead_a = __builtin_amdgcn_readlane((int)a.alive, l0) != 0;
+    bool same_a = true, same_b = true;
+    int q = 0, off = 0, lvl = 1;
+#pragma unroll
+    for (int j = 0; j < MIR_MAX_DEPTH && j < MAXD; ++j) {
+        if (j < k) {
+            const int sj = __builtin_amdgcn_readlane(lead_a ? ma[j] : mb[j], l0);
+            if (sj < p.nS) return ~0ull;  // a sphere bounce: no linear mirror
+            same_a = same_a && ma[j] == sj;
+            same_b = same_b && mb[j] == sj;
+            q = q * p.nW + (sj - p.nS);
+            if (j > 0) off += lvl;
+            lvl *= p.nW;
+        }
+    }
+    if (uniform64(__ballot((a.alive && !same_a) || (b.alive && !same_b))) != 0) return ~0ull;
+    const int l = threadIdx.x & 63;
+    const PrimBox* boxes = p.mbox + (off + q) * p.nbox;
+    const uint64_t raw = *reinterpret_cast<const uint64_t*>(boxes + (l < p.nbox ? l : 0));
+    return box_keep16(l < p.nbox ? raw : 0x80007fff80007fffull, t);
+}
+
+/* trace_pixel_d<PATH64>'s per-pixel work after the scan of segment k (the lambda's body). */
+template <bool SUN, int MAXD>
+__device__ __forceinline__ void pair_after_scan(const KParams& p, PxS<MAXD>& s, float* st_s,
+                                                float* st_k, int* st_m, const HitD& h, int k,
+                                                int& segs) {
+    if (!s.alive) return;
+    ++segs;
+    const bool last = k >= p.depth || k >= MAXD;  // remaining_iterations <= 0 (main.cpp:105)
+    if (last || h.slot < 0) {  // the path's last segment: colour only, in fp32
+        if (h.slot < 0) {
+            s.c = sky32(s.r.d);
+        } else {
+            const f3 nv32 = fnormalize(tof(s.r.d));
+            const d3 pos = s.r.o + s.r.d * h.dist;
+            f3 N32;
+            if (h.slot < p.nS) {
+                const double* S = p.s64[h.slot >> 2].v[h.slot & 3];
+                N32 = tof((s.r.o + s.r.d * h.pt) - D3(S[0], S[1], S[2]));
+            } else {
+                N32 = tof(ld3(p.w64[h.slot - p.nS].n));
+            }
+            const DevMat32& m32 = p.mat32[h.slot];
+            const float2 sh = shade_f(m32, tof(pos), fnormalize(N32), nv32, SUN);
+            s.c = local_color_f(m32, sh.x, sh.y, SUN);
+        }
+        s.alive = false;
+        return;
+    }
+    const double rdl = rcp_refined(s.r.dlen);
+    const d3 nv = div3(s.r.d, s.r.dlen, rdl);  // normalize(d)
+    const d3 pos = s.r.o + s.r.d * h.dist;     // main.cpp:99
+    d3 N;
+    if (h.slot < p.nS) {
+        const double* S = p.s64[h.slot >> 2].v[h.slot & 3];
+        N = (s.r.o + s.r.d * h.pt) - D3(S[0], S[1], S[2]);  // un-normalised, length r
+    } else {
+        N = ld3(p.w64[h.slot - p.nS].n);
+    }
+    const d3 nn = h.slot < p.nS ? normalize_e(N) : ld3(p.wnn[h.slot - p.nS]);
+    const float2 sh = shade_f(p.mat32[h.slot], tof(pos), tof(nn), tof(nv), SUN);
+    st_s[k] = sh.x;
+    st_k[k] = sh.y;
+    st_m[k] = h.slot;
+    s.n = k + 1;
+    const double cc = 2 * dot(nv, nn);
+    s.r = make_ray(pos + N * .0001, nv - nn * cc);  // main.cpp:111-113
+}
+
+template <bool SUN, int MAXD>
+__device__ __forceinline__ void trace_pair_p64(const KParams& p, int x, int i, bool va, bool vb,
+                                               int& segs, uint64_t& t_start, f3& ca, f3& cb) {
+    const d3 cpos = ld3(p.pos);
+    const d3 pca = (ld3(p.tl) + ld3(p.dx) * (double)x) + ld3(p.dy) * (double)i;  // main.cpp:132
+    const d3 pcb = (ld3(p.tl) + ld3(p.dx) * (double)(x + 8)) + ld3(p.dy) * (double)i;
+    const uint64_t braw = box_load_primary(p);
+    PxS<MAXD> a, b;
+    float as_[MAXD], ak_[MAXD], bs_[MAXD], bk_[MAXD];
+    int am_[MAXD], bm_[MAXD];
+    a.r = make_ray_lazy(cpos, cpos - pca);  // main.cpp:133-134
+    b.r = make_ray_lazy(cpos, cpos - pcb);
+    a.alive = va;
+    b.alive = vb;
+    a.n = b.n = 0;
+    a.c = b.c = F3(0.f, 0.f, 0.f);
+    t_start = RT_STAMP ? __builtin_amdgcn_s_memtime() : 0;
+    if (RT_BOX_SCHED_BARRIER) __builtin_amdgcn_sched_barrier(0);
+    const TileO tile = tile_origin(x, i);
+    uint64_t keep = box_keep16(braw, tile);
+    if (p.nbox == 0) keep = ~0ull;
+    if (keep == 0) {  // every primary ray of the 16x8 tile misses (sky fast path)
+        if (va) {
+            ++segs;
+            a.c = sky32(a.r.d);
+        }
+        if (vb) {
+            ++segs;
+            b.c = sky32(b.r.d);
+        }
+        ca = a.c;
+        cb = b.c;
+        return;
+    }
+    ray_terms(a.r);
+    ray_terms(b.r);
+    auto segment = [&](const int k) __attribute__((always_inline)) {
+        uint64_t km = ~0ull;
+        if (k == 0 && p.nbox > 0) km = keep;
+        if (k >= 1 && k <= p.mir_depth) km = mirror_keep_pair<MAXD>(p, a, b, am_, bm_, k, tile);
+        HitD ha = no_hit(), hb = no_hit();
+        const bool eye = k == 0 && p.eye;
+        if (km != ~0ull) {
+            if (eye)
+                scan_pair_bin<true>(p, a, b, km, ha, hb);
+            else
+                scan_pair_bin<false>(p, a, b, km, ha, hb);
+        } else {
+            if (eye)
+                scan_pair_all<true>(p, a, b, ha, hb);
+            else
+                scan_pair_all<false>(p, a, b, ha, hb);
+        }
+        pair_after_scan<SUN, MAXD>(p, a, as_, ak_, am_, ha, k, segs);
+        pair_after_scan<SUN, MAXD>(p, b, bs_, bk_, bm_, hb, k, segs);
+    };
+    int kend = 0;  // wave-uniform: bounce iterations run
+    if (__any(a.alive || b.alive)) {
+        segment(0);
+        if (!__any(a.alive || b.alive)) {
+            kend = 1;
+        } else {
+            segment(1);
+            for (int k = 2;; ++k) {
+                if (!__any(a.alive || b.alive)) {
+                    kend = k;
+                    break;
+                }
+                segment(k);
+            }
+        }
+    }
+    // unwind (main.cpp:117 via vec.cpp:45-49), innermost bounce first
+    for (int q = MAXD - 1; q >= 0; --q) {
+        if (q < kend) {
+            if (q < a.n) {
+                const DevMat32& m = p.mat32[am_[q]];
+                const f3 L = local_color_f(m, as_[q], ak_[q], SUN);
+                a.c = F3(fmaf(m.km, a.c.x - L.x, L.x), fmaf(m.km, a.c.y - L.y, L.y),
+                         fmaf(m.km, a.c.z - L.z, L.z));
+            }
+            if (q < b.n) {
+                const DevMat32& m = p.mat32[bm_[q]];
+                const f3 L = local_color_f(m, bs_[q], bk_[q], SUN);
+                b.c = F3(fmaf(m.km, b.c.x - L.x, L.x), fmaf(m.km, b.c.y - L.y, L.y),
+                         fmaf(m.km, b.c.z - L.z, L.z));
+            }
+        }
+    }
+    ca = a.c;
+    cb = b.c;
+}
+
+/* ------------------------------------------------------------------------ */
 /* fp32 throughput path                                                      */
 /* ------------------------------------------------------------------------ */
 /* fp32 sphere test (scaled form; det == 0 keeps scene.cpp:65's 2x distance).
@@ -1765,6 +2069,59 @@ k_trace(KParams p) {
 #endif
 }
 
+/* PATH64 linear scan, two pixels per lane (trace_pair_p64): tile pair bp of dispatch unit
+ * u covers tile columns 2bp and 2bp + 1 of its tile row. */
+#ifndef RT_WPE_PAIR
+#define RT_WPE_PAIR 3
+#endif
+template <bool SUN, int MAXD>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_WPE_PAIR, 8)))
+k_trace_pair(KParams p) {
+    static_assert(BLOCK == 64 && TILE_W == 8 && TILE_H == 8, "one 8x8 tile pair per wave");
+    const int u = tile_row(p, blockIdx.y, (int)gridDim.y);
+    const int ul = p.row_units_log2;
+    const int gx = (p.W + TILE_W - 1) / TILE_W;
+    const int bx = 2 * (((u & ((1 << ul) - 1)) * (int)gridDim.x) + (int)blockIdx.x);
+    const int trow = u >> ul;
+    const int lane = threadIdx.x & 63;
+    const int x = bx * TILE_W + (lane & 7);
+    const int r = trow * TILE_H + (lane >> 3);
+    const bool va = x < p.W && r < p.nrows, vb = x + 8 < p.W && r < p.nrows;
+    const int i = p.row0 + r;
+    int segs = 0;
+    uint64_t t_tile = 0;
+    f3 ca, cb;
+    trace_pair_p64<SUN, MAXD>(p, x, i, va, vb, segs, t_tile, ca, cb);
+    if (va) store_pixel(p, r, x, ca.x, ca.y, ca.z);
+    if (vb) store_pixel(p, r, x + 8, cb.x, cb.y, cb.z);
+    count_segments(p, segs);
+    if (RT_STAMP && lane == 0) {
+        // both tiles get the pair's cost (the host's row order reads per-tile costs)
+        const uint64_t c = (__builtin_amdgcn_s_memtime() - t_tile) >> 5;
+        const uint16_t c16 = (uint16_t)(c < 65535 ? c : 65535);
+        if (bx < gx) p.tile_cost[(size_t)trow * gx + bx] = c16;
+        if (bx + 1 < gx) p.tile_cost[(size_t)trow * gx + bx + 1] = c16;
+    }
+}
+template <bool SUN>
+static hipError_t launch_pair(const KParams& p, dim3 grid, hipStream_t st, hipEvent_t done) {
+    auto go = [&](auto kern) {
+        if (done)
+            hipExtLaunchKernelGGL(kern, grid, dim3(64), 0, st, nullptr, done, 0, p);
+        else
+            hipLaunchKernelGGL(kern, grid, dim3(64), 0, st, p);
+    };
+    if (p.depth <= MAXD_SMALL)
+        go(k_trace_pair<SUN, MAXD_SMALL>);
+    else if (p.depth <= MAXD_MID)
+        go(k_trace_pair<SUN, MAXD_MID>);
+    else if (p.depth <= MAXD_REF)
+        go(k_trace_pair<SUN, MAXD_REF>);
+    else
+        go(k_trace_pair<SUN, MAXD_LARGE>);
+    return hipGetLastError();
+}
+
 template <int PREC, bool SUN, bool INT_EXP, bool CULL, int MAXD>
 static void launch_one(const KParams& p, dim3 grid, hipStream_t st, hipEvent_t done) {
     if (done)
@@ -1823,6 +2180,13 @@ int launch_trace_ns(const KParams& p, int prec, void* stream, void* done_event) 
                     RT_TILE_PAIRS ? (units + 1) / 2 : units);
     hipStream_t st = static_cast<hipStream_t>(stream);
     hipEvent_t done = static_cast<hipEvent_t>(done_event);
+    if (p.pairs && prec == PREC_PATH64 && !p.wave_cull && BLOCK == 64 && !RT_TILE_PAIRS) {
+        // 16x8 pixels per wave: half the tile columns per dispatch unit
+        const int gxp = (((p.W + TILE_W - 1) / TILE_W) + 1) >> 1;
+        const dim3 gp((gxp + (1 << ul) - 1) >> ul, units);
+        return (int)((p.flags & FLAG_SUN) ? launch_pair<true>(p, gp, st, done)
+                                          : launch_pair<false>(p, gp, st, done));
+    }
     switch (prec) {
         case PREC_F64: return (int)launch_prec<PREC_F64>(p, grid, st, done);
         case PREC_F32: return (int)launch_prec<PREC_F32>(p, grid, st, done);

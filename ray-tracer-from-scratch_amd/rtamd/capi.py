@@ -52,6 +52,7 @@ RT_OPT_ROW_ORDER = 5
 RT_OPT_MIRROR_BINS = 6
 RT_OPT_BOX_CACHE = 7
 RT_OPT_ROW_FEEDBACK = 8
+RT_OPT_PIXEL_PAIRS = 9
 
 
 class rt_material(C.Structure):

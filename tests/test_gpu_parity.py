@@ -588,6 +588,74 @@ def test_row_feedback_and_explicit_orders_are_output_invariant(rend):
         rend.set_option(capi.RT_OPT_ROW_ORDER, 1)
 
 
+def _pair_ab(rend, cam, depth, flags=0, **kw):
+    """(one pixel per lane, two pixels per lane) PATH64 frames + segment counts."""
+    out = []
+    for on in (0, 1):
+        rend.set_option(capi.RT_OPT_PIXEL_PAIRS, on)
+        img, st = rend.render(cam, depth, capi.RT_PREC_PATH64, flags, capi.RT_OUT_RGB_F32,
+                              count_segments=True, **kw)
+        out.append((img, st.segments))
+    return out
+
+
+def test_pixel_pairs_bitwise(rend):
+    """RT_OPT_PIXEL_PAIRS (two pixels per lane, 16x8 pixels per wave) evaluates every test,
+    shading step and unwind of the one-pixel PATH64 kernel under shared branches with
+    predicated takes: frames and segment counts bitwise equal to the one-pixel kernel —
+    random scenes and views up to the 64-primitive tile-bin limit (walls through the camera,
+    edge-on views), ragged widths (a lane's second pixel past the row end), row bands,
+    every register-stack tier (depth 0-12), the sun extension, bins on and off, and
+    full-size c2 under the measured row order."""
+    rng = np.random.default_rng(91)
+    rend.set_option(capi.RT_OPT_WAVE_CULL_MIN_SPHERES, 2**31 - 1)  # linear scan up to 64 prims
+    try:
+        trials = [(1, 0), (0, 1), (8, 4), (8, 6), (2, 9), (4, 7), (20, 12), (40, 24), (3, 40),
+                  (16, 2)]
+        for trial, (ns, nw) in enumerate(trials * 2):
+            sc = scenes.synthetic_scene(ns, min(nw, 6), seed=int(rng.integers(1 << 30)))
+            pos = rng.uniform([-1, -3, -1], [5, 3, 2])
+            for k in range(nw - 6):
+                sc.append(_random_wall(rng, near=pos if k % 3 == 0 else None))
+            rend.set_scene(scenes.to_prims(sc))
+            vfov = float(rng.choice([20.0, 60.0, 90.0, 150.0]))
+            w = int(rng.choice([1, 9, 15, 64, 161, 240]))
+            aspect = float(rng.choice([1.0, 16 / 9, 4 / 3, 0.5]))
+            look = pos + rng.normal(size=3)
+            if trial % 4 == 3:
+                look = pos + np.array([1.0, 0.0, 0.0])
+            cam = capi.camera_init(pos, look, (0, 0, -1), vfov, aspect, float(w))
+            if cam.height <= 0:
+                continue
+            depth = int(rng.choice([0, 1, 2, 4, 6, 9, 12]))
+            r0 = int(rng.integers(0, cam.height))
+            n = int(rng.integers(1, cam.height - r0 + 1))
+            flags = capi.RT_FLAG_SUN if trial % 5 == 4 else 0
+            rend.set_option(capi.RT_OPT_TILE_BINS, 0 if trial % 7 == 6 else 1)
+            (i1, s1), (i2, s2) = _pair_ab(rend, cam, depth, flags, row0=r0, nrows=n)
+            assert s1 == s2, trial
+            assert np.array_equal(i1.view(np.uint32), i2.view(np.uint32)), trial
+        rend.set_option(capi.RT_OPT_TILE_BINS, 1)
+        rend.set_option(capi.RT_OPT_WAVE_CULL_MIN_SPHERES, 24)
+        # the bench scene at full size, measured row order (stamped frames included)
+        cfg = scenes.CONFIGS["c2"]
+        rend.set_scene(scenes.to_prims(cfg.scene()))
+        cam = capi.camera_init(**scenes.camera_args(cfg.width, cfg.height))
+        rend.set_option(capi.RT_OPT_ROW_FEEDBACK, 1)
+        (ref, s_ref), _ = _pair_ab(rend, cam, cfg.depth)
+        rend.set_option(capi.RT_OPT_PIXEL_PAIRS, 1)
+        for _ in range(4):
+            img, st = rend.render(cam, cfg.depth, capi.RT_PREC_PATH64, 0, capi.RT_OUT_RGB_F32,
+                                  count_segments=True)
+            assert st.segments == s_ref
+            assert np.array_equal(img.view(np.uint32), ref.view(np.uint32))
+    finally:
+        rend.set_option(capi.RT_OPT_PIXEL_PAIRS, 0)
+        rend.set_option(capi.RT_OPT_ROW_FEEDBACK, 32)
+        rend.set_option(capi.RT_OPT_TILE_BINS, 1)
+        rend.set_option(capi.RT_OPT_WAVE_CULL_MIN_SPHERES, 24)
+
+
 # ---------------------------------------------------------------- headless frame loop
 def _read_ppm(path):
     with open(path, "rb") as fh:

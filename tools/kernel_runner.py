@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--sun", action="store_true")
     ap.add_argument("--depth", type=int, default=-1, help="-1 = the config's depth")
     ap.add_argument("--lib", default="", help="another build of librt_amd.so (A/B)")
+    ap.add_argument("--opt", action="append", default=[],
+                    help="rt_set_option NAME=VALUE (e.g. PIXEL_PAIRS=1), repeatable")
     args = ap.parse_args()
     import torch
     dev = torch.device("cuda", 0)
@@ -28,6 +30,9 @@ def main():
     if args.lib:
         capi._lib = capi.load(os.path.abspath(args.lib))
     rend = capi.Renderer(0)
+    for o in args.opt:
+        name, val = o.split("=")
+        rend.set_option(getattr(capi, "RT_OPT_" + name), int(val))
     rend.set_scene(scenes.to_prims(cfg.scene()))
     cam = capi.camera_init(**scenes.camera_args(cfg.width, cfg.height))
     out = torch.empty((cam.height, cam.width, 3), dtype=torch.float32, device=dev)

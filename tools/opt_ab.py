@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--sun", action="store_true")
+    ap.add_argument("--depth", type=int, default=-1, help="-1 = the config's depth")
     args = ap.parse_args()
     import torch
     dev = torch.device("cuda", 0)
@@ -43,13 +44,13 @@ def main():
                 for v in vals:
                     rend.set_option(opt, v)
                     for _ in range(2):
-                        rend.render_device(cam, cfg.depth, out.data_ptr(), pc, flags, 0,
+                        rend.render_device(cam, (cfg.depth if args.depth < 0 else args.depth), out.data_ptr(), pc, flags, 0,
                                            stream=stream.cuda_stream)
                     e0 = torch.cuda.Event(enable_timing=True)
                     e1 = torch.cuda.Event(enable_timing=True)
                     e0.record(stream)
                     for _ in range(args.reps):
-                        rend.render_device(cam, cfg.depth, out.data_ptr(), pc, flags, 0,
+                        rend.render_device(cam, (cfg.depth if args.depth < 0 else args.depth), out.data_ptr(), pc, flags, 0,
                                            stream=stream.cuda_stream)
                     e1.record(stream)
                     torch.cuda.synchronize()
