@@ -18,6 +18,13 @@ layout of BASELINE config 4.
 Rays = segments = closest-hit queries (primary + reflection), counted exactly by the
 kernel in an untimed census launch.
 
+Order of a run: census; the side measurements (per-precision sweep, sun extension, moving
+camera — before the timed region, so it starts on a GPU at its running clock rather than
+on the ramp out of idle); W warmup steps; K timed steps; the one-stream kernel time.  The
+warmup and timed steps of frames mode are enqueued by one rt_render_device_frames call
+each (every frame's own host work and launch, as a C++ frame loop over rt_render_device
+would do them, without Python's per-call overhead).
+
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2] [--precision mixed]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 """
@@ -203,6 +210,23 @@ def main() -> int:
             launch(slot=nstep[0] % fif)
             nstep[0] += 1
 
+    out_ptrs = [o.data_ptr() for o in outs]
+    st_ptrs = [s_.cuda_stream for s_ in streams]
+
+    def run_steps(n: int):
+        """n consecutive steps: frames mode enqueues them with ONE C-ABI call
+        (rt_render_device_frames: each frame's own host work and launch, minus the Python
+        per-call overhead, so the host stays ahead of the GPU as a C++ frame loop would)."""
+        if tiled is not None:
+            for _ in range(n):
+                step()
+            return
+        k = nstep[0] % fif
+        rend.render_device_frames([cam], depth, out_ptrs[k:] + out_ptrs[:k], prec, flags,
+                                  out_fmt, row0=row0, nrows=nrows,
+                                  streams=st_ptrs[k:] + st_ptrs[:k], nframes=n)
+        nstep[0] += n
+
     def join_streams():
         # stream 0 waits for every other stream's work (the end-of-region event is then
         # behind every frame of the region)
@@ -218,57 +242,28 @@ def main() -> int:
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
     total_segs = int(tot.item())
 
-    for _ in range(args.warmup):
-        step()
-    if tiled is not None:
-        tiled.drain()
-    barrier()
-    torch.cuda.synchronize(dev)
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
-        step()
-    if tiled is not None:
-        tiled.drain()
-    join_streams()
-    ev1.record(stream)
-    torch.cuda.synchronize(dev)
-    barrier()
-    t1 = time.perf_counter()
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    elapsed_s = float(elapsed.item())
-    stream_ms = ev0.elapsed_time(ev1) / args.steps
-
-    # per-launch kernel time: one stream, launches back to back (HIP events on that stream)
-    ek0 = torch.cuda.Event(enable_timing=True)
-    ek1 = torch.cuda.Event(enable_timing=True)
-    nk = max(10, args.steps)
-    ek0.record(stream)
-    for _ in range(nk):
-        launch()
-    ek1.record(stream)
-    torch.cuda.synchronize(dev)
-    kernel_ms = ek0.elapsed_time(ek1) / nk
-
+    # Side measurements (per-precision kernel sweep, sun extension, moving camera) run
+    # BEFORE the warmup and the timed region, on every rank (rank 0 reports them).  They
+    # are measurements of their own; running them first also means the timed region
+    # starts on a GPU at its sustained clock, as inside a running frame loop, rather than
+    # on the ramp out of idle (tools/ramp_probe.py: frames 4-255 after idle run ~7%
+    # slower than later ones, so a 20-step region would measure the ramp).
+    nsw = 200
     sweep = {}
     sun_ext = None
-    if rank == 0 and not args.no_sweep:
+    if not args.no_sweep:
         for pname, pc in capi.PRECISIONS.items():
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
             rend.render_device(cam, depth, out.data_ptr(), pc, flags, capi.RT_OUT_RGB_F32,
                                row0=row0, nrows=nrows, stream=stream.cuda_stream)
             e0.record(stream)
-            for _ in range(nk):
+            for _ in range(nsw):
                 rend.render_device(cam, depth, out.data_ptr(), pc, flags, capi.RT_OUT_RGB_F32,
                                    row0=row0, nrows=nrows, stream=stream.cuda_stream)
             e1.record(stream)
             torch.cuda.synchronize(dev)
-            kms = e0.elapsed_time(e1) / nk
+            kms = e0.elapsed_time(e1) / nsw
             sweep[pname] = {"kernel_ms": round(kms, 4),
                             "mrays_per_s": round(my_segs / (kms * 1e-3) / 1e6, 1),
                             "dtype": DTYPE[pname], "parity": PARITY[pname]}
@@ -280,20 +275,20 @@ def main() -> int:
             rend.render_device(cam, depth, out.data_ptr(), prec, capi.RT_FLAG_SUN,
                                capi.RT_OUT_RGB_F32, row0=row0, nrows=nrows, stream=stream.cuda_stream)
             e0.record(stream)
-            for _ in range(nk):
+            for _ in range(nsw):
                 rend.render_device(cam, depth, out.data_ptr(), prec, capi.RT_FLAG_SUN,
                                    capi.RT_OUT_RGB_F32, row0=row0, nrows=nrows,
                                    stream=stream.cuda_stream)
             e1.record(stream)
             torch.cuda.synchronize(dev)
-            kms = e0.elapsed_time(e1) / nk
+            kms = e0.elapsed_time(e1) / nsw
             sun_ext = {"precision": args.precision, "kernel_ms": round(kms, 4),
                        "mrays_per_s": round(my_segs / (kms * 1e-3) / 1e6, 1),
                        "parity": "sun term is build-defined (constants main.cpp:18-19, unused "
                                  "by the reference): pinned to the oracle, not the reference"}
 
     moving = None
-    if rank == 0 and not args.no_sweep and args.mode == "frames":
+    if not args.no_sweep and args.mode == "frames":
         # the measured tile-row order on a camera that moves every frame (a fly-through of
         # 200 frames, 0.01 scene units per frame toward the scene — rays travel toward +x,
         # main.cpp:133): the order is refreshed every RT_OPT_ROW_FEEDBACK frames, so it
@@ -323,6 +318,48 @@ def main() -> int:
                 best = ms if best is None else min(best, ms)
             moving[f"ms_per_frame_row_feedback_{fb}"] = round(best, 4)
         rend.set_option(capi.RT_OPT_ROW_FEEDBACK, args.row_feedback)
+
+    # the moving camera left the row feedback holding another view's order: drop it (with
+    # any snapshot still in flight), so the first warmup frame samples this camera afresh.
+    # (Measured: priming it from isolated frames instead — one or more synchronous census
+    # frames — gives orders 4-8% slower for frames in flight than a sample taken among
+    # them; more back-to-back samples inside a 20-step region cost more than they gain.)
+    rend.set_option(capi.RT_OPT_ROW_FEEDBACK, 0)
+    rend.set_option(capi.RT_OPT_ROW_FEEDBACK, args.row_feedback)
+
+    run_steps(args.warmup)
+    if tiled is not None:
+        tiled.drain()
+    barrier()
+    torch.cuda.synchronize(dev)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    run_steps(args.steps)
+    if tiled is not None:
+        tiled.drain()
+    join_streams()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    barrier()
+    t1 = time.perf_counter()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed_s = float(elapsed.item())
+    stream_ms = ev0.elapsed_time(ev1) / args.steps
+
+    # per-launch kernel time: one stream, launches back to back (HIP events on that stream)
+    ek0 = torch.cuda.Event(enable_timing=True)
+    ek1 = torch.cuda.Event(enable_timing=True)
+    nk = max(10, args.steps)
+    ek0.record(stream)
+    rend.render_device_frames([cam], depth, [out.data_ptr()], prec, flags, out_fmt, row0=row0,
+                              nrows=nrows, streams=[stream.cuda_stream], nframes=nk)
+    ek1.record(stream)
+    torch.cuda.synchronize(dev)
+    kernel_ms = ek0.elapsed_time(ek1) / nk
 
     result = None
     if rank == 0:

@@ -177,10 +177,17 @@ enum rt_option {
                                          band or scene) a snapshot is copied back behind the
                                          kernel, and later renders of the same band dispatch
                                          tile rows heaviest-first by it (scheduling only);
-                                         0 = off.  Output is identical. */
-    RT_OPT_PIXEL_PAIRS = 9            /* 1: RT_PREC_PATH64 renders without the wave cull
+                                         0 = off.  Setting it (any value) drops the order
+                                         and any snapshot still in flight.  Output is
+                                         identical. */
+    RT_OPT_PIXEL_PAIRS = 9,           /* 1: RT_PREC_PATH64 renders without the wave cull
                                          trace two pixels per lane (16x8 pixels per
                                          wave); 0 (default) = one.  Output is identical. */
+    RT_OPT_ROW_FEEDBACK_WARM = 10     /* K >= 0 (default 0): after a new band or scene,
+                                         RT_OPT_ROW_FEEDBACK takes K more snapshots back to
+                                         back (each once the previous one has landed)
+                                         before its interval applies.  Output is
+                                         identical. */
 };
 int rt_set_option(rt_ctx* ctx, int32_t option, int64_t value);
 
@@ -209,6 +216,17 @@ int rt_render(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nrows, in
 int rt_render_device(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nrows,
                      int32_t depth, int32_t precision, uint32_t flags, int32_t out_format,
                      void* d_out, uint64_t* d_segments, void* stream);
+
+/* A batch of frames of the frame loop (main.cpp:250-375 renders one frame per iteration),
+ * enqueued by one call: frame f (0 <= f < nframes) renders cams[f % ncams] into
+ * d_outs[f % nouts] on streams[f % nstreams] (NULL entries = the ctx's stream), exactly
+ * as nframes rt_render_device calls in that order would — each frame's own host work
+ * (pixel boxes, row order) and launch — without the caller's per-call overhead.  No
+ * synchronisation; stops at the first failing frame and returns its status. */
+int rt_render_device_frames(rt_ctx* ctx, const rt_camera* cams, int32_t ncams, int32_t row0,
+                            int32_t nrows, int32_t depth, int32_t precision, uint32_t flags,
+                            int32_t out_format, void* const* d_outs, int32_t nouts,
+                            void* const* streams, int32_t nstreams, int32_t nframes);
 
 /* ---- host helpers (restatements the host side of rt_scene needs) -------- */
 /* Camera::init (scene.cpp:80-106) in fp64: fills cam from the Camera fields.

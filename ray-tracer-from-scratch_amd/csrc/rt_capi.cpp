@@ -76,15 +76,23 @@ struct rt_ctx {
     struct Band {
         int32_t W = -1, row0 = -1, nrows = -1;
         unsigned long long scene_gen = 0;
+        unsigned fb_epoch = 0;  // rt_set_option(RT_OPT_ROW_FEEDBACK) starts a new epoch
         bool operator==(const Band& o) const {
-            return W == o.W && row0 == o.row0 && nrows == o.nrows && scene_gen == o.scene_gen;
+            return W == o.W && row0 == o.row0 && nrows == o.nrows && scene_gen == o.scene_gen &&
+                   fb_epoch == o.fb_epoch;
         }
     };
+    unsigned fb_epoch = 0;  // a snapshot still in flight from an older epoch is not used
     Band cost_band;                // band of the pending snapshot
     Band fb_band;                  // band fb_perm was computed for
     std::vector<int16_t> fb_perm;  // over dispatch units: 2^fb_units_log2 per tile row
     int fb_units_log2 = 0;
     int since_snapshot = 0;
+    // RT_OPT_ROW_FEEDBACK_WARM: after a new band or scene, this many further snapshots are
+    // taken back to back (each as soon as the previous one has landed) before the interval
+    // applies, so the order settles within a few frames instead of a few intervals
+    int fb_warm = 0;
+    int warm_left = 0;
     // the per-frame boxes depend only on the scene, the camera, the row band and the
     // options: a render with the same inputs as the previous one reuses them (the host
     // part of a frame is ~60 us with mirror chains, more than the kernel at c2)
@@ -981,9 +989,14 @@ int rt_set_option(rt_ctx* ctx, int32_t option, int64_t value) {
             if (value != 0 && value != 1) return RT_ERR_INVALID_ARG;
             ctx->pixel_pairs = value == 1;
             return RT_OK;
+        case RT_OPT_ROW_FEEDBACK_WARM:
+            if (value < 0 || value > 1000) return RT_ERR_INVALID_ARG;
+            ctx->fb_warm = (int)value;
+            return RT_OK;
         case RT_OPT_ROW_FEEDBACK:
             if (value < 0 || value > 1000000) return RT_ERR_INVALID_ARG;
             ctx->feedback = (int)value;
+            ctx->fb_epoch++;  // orders and snapshots taken so far belong to the old setting
             if (value == 0) {
                 ctx->fb_perm.clear();
                 ctx->fb_band = rt_ctx::Band{};
@@ -1056,7 +1069,7 @@ static int prepare_rows(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t
                         hipStream_t st, rt::KParams& p) {
     const int gy = (nrows + rt::TILE_H - 1) / rt::TILE_H;
     const int per_row = ((cam->width + rt::TILE_W - 1) / rt::TILE_W) * (rt::BLOCK / 64);
-    const rt_ctx::Band band{cam->width, row0, nrows, ctx->scene_gen};
+    const rt_ctx::Band band{cam->width, row0, nrows, ctx->scene_gen, ctx->fb_epoch};
     if (ctx->cost_pending && hipEventQuery(ctx->ev_cost) == hipSuccess) {
         ctx->cost_pending = false;
         const rt_ctx::Band& b = ctx->cost_band;
@@ -1084,7 +1097,13 @@ static int prepare_rows(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t
     p.tile_cost = nullptr;
     if (ctx->feedback <= 0 || !ctx->row_perm.empty() || gy > rt::ROW_PERM_MAX || ctx->cost_pending)
         return RT_OK;
-    if (++ctx->since_snapshot < ctx->feedback && ctx->fb_band == band) return RT_OK;
+    if (!(ctx->fb_band == band)) {
+        ctx->warm_left = ctx->fb_warm;  // a new band or scene: the first snapshot, then the warm ones
+    } else if (ctx->warm_left > 0) {
+        ctx->warm_left--;
+    } else if (++ctx->since_snapshot < ctx->feedback) {
+        return RT_OK;
+    }
     const size_t need = (size_t)gy * per_row;
     if (need > ctx->d_cost_cap) {
         // grow (rare): nothing in flight may still use the old buffers
@@ -1109,7 +1128,7 @@ static int prepare_rows(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t
 static int snapshot_costs(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nrows,
                           hipStream_t st, const rt::KParams& p) {
     if (!p.tile_cost) return RT_OK;
-    const rt_ctx::Band band{cam->width, row0, nrows, ctx->scene_gen};
+    const rt_ctx::Band band{cam->width, row0, nrows, ctx->scene_gen, ctx->fb_epoch};
     const int gy = (nrows + rt::TILE_H - 1) / rt::TILE_H;
     const size_t n = (size_t)gy * ((cam->width + rt::TILE_W - 1) / rt::TILE_W) * (rt::BLOCK / 64);
     RT_HIP(ctx, hipMemcpyAsync(ctx->h_cost, ctx->d_cost, n * sizeof(uint16_t),
@@ -1153,6 +1172,22 @@ int rt_render_device(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nr
     st = snapshot_costs(ctx, cam, row0, nrows, hs, p);
     HP(4);
     return st;
+}
+
+int rt_render_device_frames(rt_ctx* ctx, const rt_camera* cams, int32_t ncams, int32_t row0,
+                            int32_t nrows, int32_t depth, int32_t precision, uint32_t flags,
+                            int32_t out_format, void* const* d_outs, int32_t nouts,
+                            void* const* streams, int32_t nstreams, int32_t nframes) {
+    if (!ctx || !cams || ncams <= 0 || !d_outs || nouts <= 0 || nframes < 0 ||
+        (nstreams > 0 && !streams) || nstreams < 0)
+        return RT_ERR_INVALID_ARG;
+    for (int32_t f = 0; f < nframes; f++) {
+        void* st = nstreams > 0 ? streams[f % nstreams] : nullptr;
+        const int e = rt_render_device(ctx, &cams[f % ncams], row0, nrows, depth, precision,
+                                       flags, out_format, d_outs[f % nouts], nullptr, st);
+        if (e != RT_OK) return e;
+    }
+    return RT_OK;
 }
 
 int rt_render(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nrows, int32_t depth,

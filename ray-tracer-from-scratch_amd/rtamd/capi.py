@@ -53,6 +53,7 @@ RT_OPT_MIRROR_BINS = 6
 RT_OPT_BOX_CACHE = 7
 RT_OPT_ROW_FEEDBACK = 8
 RT_OPT_PIXEL_PAIRS = 9
+RT_OPT_ROW_FEEDBACK_WARM = 10
 
 
 class rt_material(C.Structure):
@@ -110,6 +111,10 @@ SIGNATURES = [
     ("rt_render_device", C.c_int,
      [C.c_void_p, C.POINTER(rt_camera), C.c_int32, C.c_int32, C.c_int32, C.c_int32,
       C.c_uint32, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]),
+    ("rt_render_device_frames", C.c_int,
+     [C.c_void_p, C.POINTER(rt_camera), C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+      C.c_uint32, C.c_int32, C.POINTER(C.c_void_p), C.c_int32, C.POINTER(C.c_void_p),
+      C.c_int32, C.c_int32]),
     ("rt_camera_init", C.c_int,
      [_dbl3, _dbl3, _dbl3, C.c_double, C.c_double, C.c_double, C.POINTER(rt_camera)]),
     ("rt_out_bytes_per_pixel", C.c_int32, [C.c_int32]),
@@ -288,3 +293,18 @@ class Renderer:
                                         flags, out_format, C.c_void_p(d_out),
                                         C.c_void_p(d_segments or None),
                                         C.c_void_p(stream or None)), self.ctx)
+
+    def render_device_frames(self, cams, depth: int, d_outs, precision: int = RT_PREC_F64,
+                             flags: int = 0, out_format: int = RT_OUT_RGB_F32, row0: int = 0,
+                             nrows: int | None = None, streams=(), nframes: int = 1) -> None:
+        """rt_render_device_frames: frame f renders cams[f % len(cams)] into
+        d_outs[f % len(d_outs)] on streams[f % len(streams)] (raw pointers), one call."""
+        cams = list(cams)
+        if nrows is None:
+            nrows = cams[0].height - row0
+        ca = (rt_camera * len(cams))(*cams)
+        outs = (C.c_void_p * len(d_outs))(*[C.c_void_p(o) for o in d_outs])
+        sts = (C.c_void_p * max(1, len(streams)))(*[C.c_void_p(x or None) for x in streams])
+        check(self.lib.rt_render_device_frames(self.ctx, ca, len(cams), row0, nrows, depth,
+                                               precision, flags, out_format, outs, len(d_outs),
+                                               sts, len(streams), nframes), self.ctx)

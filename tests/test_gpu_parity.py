@@ -588,6 +588,32 @@ def test_row_feedback_and_explicit_orders_are_output_invariant(rend):
         rend.set_option(capi.RT_OPT_ROW_ORDER, 1)
 
 
+def test_render_device_frames_equals_per_frame_calls(rend):
+    """rt_render_device_frames (the bench's frame loop in one call): frame f renders
+    cams[f % 2] into buffer f % 3 on stream f % 3 — each buffer ends bitwise equal to a
+    single render of the camera of its last frame; bad arguments are rejected."""
+    import torch
+    dev = torch.device("cuda", 0)
+    sc = scenes.synthetic_scene(8, 4)
+    rend.set_scene(scenes.to_prims(sc))
+    ca = scenes.camera_args(160, 90)
+    cams = [capi.camera_init(**ca)]
+    a = dict(ca)
+    a["position"] = (ca["position"][0] + 0.3, ca["position"][1], ca["position"][2])
+    cams.append(capi.camera_init(**a))
+    refs = [rend.render(c, 4, capi.RT_PREC_PATH64, 0, capi.RT_OUT_RGB_F32)[0] for c in cams]
+    outs = [torch.zeros((90, 160, 3), dtype=torch.float32, device=dev) for _ in range(3)]
+    sts = [torch.cuda.Stream(dev) for _ in range(3)]
+    rend.render_device_frames(cams, 4, [o.data_ptr() for o in outs], capi.RT_PREC_PATH64,
+                              streams=[s.cuda_stream for s in sts], nframes=7)
+    torch.cuda.synchronize()
+    last_cam = {0: 0, 1: 0, 2: 1}  # frames 6, 4, 5
+    for b, o in enumerate(outs):
+        assert np.array_equal(o.cpu().numpy().view(np.uint32), refs[last_cam[b]].view(np.uint32))
+    with pytest.raises(capi.RTError):
+        rend.render_device_frames(cams, 4, [], capi.RT_PREC_PATH64, nframes=1)
+
+
 def _pair_ab(rend, cam, depth, flags=0, **kw):
     """(one pixel per lane, two pixels per lane) PATH64 frames + segment counts."""
     out = []
