@@ -8,7 +8,7 @@ already resident on the device.  With N ranks the batch is N frames of a camera
 fly-through (rank r renders frame r: the camera moved r steps forward the way
 Camera::forward moves it, scene.cpp:121) — frames are independent units, sharded with
 no data-path collective, so `scaling` is "weak".  Consecutive frames of a rank go to
-`--frames-in-flight` output buffers on as many streams (default 3, a triple-buffered frame
+`--frames-in-flight` output buffers on as many streams (default 2, a double-buffered frame
 loop): every frame is rendered in full, and one frame's last (heaviest) waves overlap the
 next frame's first instead of leaving the GPU draining between launches; `kernel_ms` is
 the one-frame-at-a-time kernel duration.  `--mode tiled` instead splits ONE
@@ -116,7 +116,7 @@ def main() -> int:
     ap.add_argument("--out", default="rgb_f32", choices=["rgb_f32", "rgba8"],
                     help="timed output format: linear fp32 RGB (12 B/px, parity buffer) or the "
                          "clamp+truncate RGBA8 epilogue (4 B/px; cuts the tiled gather 3x)")
-    ap.add_argument("--frames-in-flight", type=int, default=3,
+    ap.add_argument("--frames-in-flight", type=int, default=2,
                     help="frames mode: consecutive frames go to F output buffers on F streams "
                          "(a triple-buffered frame loop), so one frame's last waves overlap the "
                          "next frame's first; 1 = one stream, frames back to back")
