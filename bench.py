@@ -320,10 +320,13 @@ def main() -> int:
         rend.set_option(capi.RT_OPT_ROW_FEEDBACK, args.row_feedback)
 
     # the moving camera left the row feedback holding another view's order: drop it (with
-    # any snapshot still in flight), so the first warmup frame samples this camera afresh.
-    # (Measured: priming it from isolated frames instead — one or more synchronous census
-    # frames — gives orders 4-8% slower for frames in flight than a sample taken among
-    # them; more back-to-back samples inside a 20-step region cost more than they gain.)
+    # any snapshot still in flight), so the first warmup frame samples this camera afresh,
+    # with frames in flight as the timed steps run them.  (Measured with 20-step regions,
+    # interleaved on one box: an order sampled from isolated launches — synchronous census
+    # frames, or the sweep's back-to-back frames — runs the frames-in-flight loop 4-8%
+    # slower on average and erratically (78-120 Grays/s); one sampled among frames in
+    # flight gives 116-121; more back-to-back samples inside a 20-step region cost more than
+    # they gain.)
     rend.set_option(capi.RT_OPT_ROW_FEEDBACK, 0)
     rend.set_option(capi.RT_OPT_ROW_FEEDBACK, args.row_feedback)
 
