@@ -141,10 +141,19 @@ def main() -> int:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    # RT_BENCH_BACKEND=gloo: rehearsal of the N-rank code path on fewer GPUs than ranks
+    # (ranks share devices round-robin; RCCL refuses two ranks on one GPU).  Not a
+    # measurement: the driver's multi-GPU runs use the default, RCCL ("nccl").
+    backend = os.environ.get("RT_BENCH_BACKEND", "nccl")
+    if backend == "gloo":
+        local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     def barrier():
         if world > 1:
@@ -408,6 +417,7 @@ def main() -> int:
                 "host_box_cache": bool(args.box_cache),
                 "row_feedback": args.row_feedback,
                 "frames_in_flight": fif,
+                "backend": backend if world > 1 else None,
             },
             "ms_per_frame": round(ms_step / frames_per_step if args.mode == "frames" else ms_step, 4),
             "mpx_per_s": round(px_step * args.steps / elapsed_s / 1e6, 2),
