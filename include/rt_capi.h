@@ -183,11 +183,16 @@ enum rt_option {
     RT_OPT_PIXEL_PAIRS = 9,           /* 1: RT_PREC_PATH64 renders without the wave cull
                                          trace two pixels per lane (16x8 pixels per
                                          wave); 0 (default) = one.  Output is identical. */
-    RT_OPT_ROW_FEEDBACK_WARM = 10     /* K >= 0 (default 0): after a new band or scene,
+    RT_OPT_ROW_FEEDBACK_WARM = 10,    /* K >= 0 (default 0): after a new band or scene,
                                          RT_OPT_ROW_FEEDBACK takes K more snapshots back to
                                          back (each once the previous one has landed)
                                          before its interval applies.  Output is
                                          identical. */
+    RT_OPT_WALL_ORDER = 11            /* 1: the primary scan visits the walls nearest to
+                                         the camera first (per frame), so a wall behind the
+                                         best hit skips its bounds test; 0 (default) = scene
+                                         order (measured: c2 +1% with the order).  Output is
+                                         identical (wall ties compare scene indices). */
 };
 int rt_set_option(rt_ctx* ctx, int32_t option, int64_t value);
 

@@ -5,6 +5,9 @@
  * timing events and a staging buffer for host-output renders.  No exception crosses
  * the boundary; every entry point returns an rt_status.
  */
+#ifndef RT_WALL_ORDER_DEFAULT   // build-time default of RT_OPT_WALL_ORDER (A/B builds)
+#define RT_WALL_ORDER_DEFAULT 0
+#endif
 #ifndef RT_PIXEL_PAIRS_DEFAULT  // build-time default of RT_OPT_PIXEL_PAIRS (A/B builds)
 #define RT_PIXEL_PAIRS_DEFAULT 0
 #endif
@@ -57,6 +60,7 @@ struct rt_ctx {
     unsigned long long* d_stats = nullptr;
     int wave_cull_min = 24;  // spheres from which the wave cull pays (tools/sweep.py)
     bool eye_tables = true;  // RT_OPT_EYE_TABLES
+    bool wall_order = RT_WALL_ORDER_DEFAULT;  // RT_OPT_WALL_ORDER
     bool tile_bins = true;   // RT_OPT_TILE_BINS
     bool row_order = true;   // RT_OPT_ROW_ORDER
     bool mirror_bins = true; // RT_OPT_MIRROR_BINS
@@ -590,6 +594,34 @@ rt::KParams make_params(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, i
             p.eye_w[w] = (P[0] - o[0]) * n[0] + (P[1] - o[1]) * n[1] + (P[2] - o[2]) * n[2];  // scene.cpp:10
         }
     }
+    // primary scan's wall order: nearest rectangle to the camera first, so the wall t-skip
+    // (t > best) drops the bounds test of the walls it occludes.  Any order gives the
+    // reference's winner (wall ties compare scene indices, rt_trace.hip wall_exact).
+    p.wall_order_n = 0;
+    p.wall_order = 0;
+    if (ctx->wall_order && ctx->sc.nW > 1 && ctx->sc.nW <= 16) {
+        const double* o = cam->position;
+        double key[16];
+        int ord[16];
+        for (int w = 0; w < ctx->sc.nW; w++) {
+            const double* Wd = &ctx->sc.h_wal[14 * w];
+            const double *Pw = Wd, *X = Wd + 6, *Y = Wd + 9;
+            const double v[3] = {o[0] - Pw[0], o[1] - Pw[1], o[2] - Pw[2]};
+            // closest point of the rectangle P + a X + b Y (a in [0, len], b in [0, wid])
+            const double a = std::min(std::max(v[0] * X[0] + v[1] * X[1] + v[2] * X[2], 0.0), Wd[12]);
+            const double b = std::min(std::max(v[0] * Y[0] + v[1] * Y[1] + v[2] * Y[2], 0.0), Wd[13]);
+            double d2 = 0.0;
+            for (int k = 0; k < 3; k++) {
+                const double e = v[k] - a * X[k] - b * Y[k];
+                d2 += e * e;
+            }
+            key[w] = std::isnan(d2) ? 1e300 : d2;
+            ord[w] = w;
+        }
+        std::stable_sort(ord, ord + ctx->sc.nW, [&](int x, int y) { return key[x] < key[y]; });
+        for (int k = 0; k < ctx->sc.nW; k++) p.wall_order |= (uint64_t)ord[k] << (4 * k);
+        p.wall_order_n = ctx->sc.nW;
+    }
     // per-frame boxes, or the previous render's when its inputs were the same
     rt_ctx::BoxCache& bc = ctx->box_cache;
     const int32_t opts = (ctx->tile_bins ? 1 : 0) | (ctx->row_order ? 2 : 0) | (ctx->mirror_bins ? 4 : 0);
@@ -964,6 +996,10 @@ int rt_set_option(rt_ctx* ctx, int32_t option, int64_t value) {
             return RT_OK;
         case RT_OPT_STATS_DEVICE_PTR:
             ctx->d_stats = reinterpret_cast<unsigned long long*>(static_cast<intptr_t>(value));
+            return RT_OK;
+        case RT_OPT_WALL_ORDER:
+            if (value != 0 && value != 1) return RT_ERR_INVALID_ARG;
+            ctx->wall_order = value == 1;
             return RT_OK;
         case RT_OPT_EYE_TABLES:
             if (value != 0 && value != 1) return RT_ERR_INVALID_ARG;

@@ -157,7 +157,9 @@ struct KParams {
     PrimBox mbox[MIR_MAX_BOXES];  // [sequence][slot j]: primitive j through the camera
                                   // mirrored along the sequence (see above)
     int32_t eye;                        // eye tables below valid
-    int32_t pad_eye;
+    int32_t wall_order_n;               // walls in wall_order (== nW), 0 = index order
+    uint64_t wall_order;                // primary scan's wall visiting order, 4 bits per
+                                        // wall slot, nearest to the camera first (host)
     double eye_s[EYE_MAX_S][4];         // sphere s: {oc.x, oc.y, oc.z, |oc|^2 - r^2}
     double eye_w[EYE_MAX_W];            // wall w: dot(P - pos, n)
 };

@@ -82,6 +82,12 @@
 #ifndef RT_BOX_SCHED_BARRIER
 #define RT_BOX_SCHED_BARRIER 1
 #endif
+#ifndef RT_WALL_ORDER      // 1: the primary scan visits walls in the host's per-frame order
+#define RT_WALL_ORDER 1    // (nearest to the camera first) when KParams::wall_order is set
+#endif
+#ifndef RT_WALL_ORDER      // 1: the primary scan visits walls in the host's per-frame order
+#define RT_WALL_ORDER 1    // (nearest to the camera first) when KParams::wall_order is set
+#endif
 #ifndef RT_WALL_PAIRS      // exact wall tests two at a time in one basic block (ILP)
 #define RT_WALL_PAIRS 0    // A/B: +10% at c2 (lost t-skip, +16 VGPRs), off
 #endif
@@ -771,6 +777,19 @@ __device__ __forceinline__ HitD closest_hit_bin(const KParams& p, const RayD& r,
         }
     }
     uint64_t wm = p.nS >= 64 ? 0 : keep >> p.nS;
+    if (EYE && RT_WALL_ORDER && p.wall_order_n == p.nW) {
+        // primary rays: the walls nearest to the camera first (host order, KParams::
+        // wall_order), so a wall behind the best hit skips its bounds test (t-skip); any
+        // order finds the reference's winner (wall ties compare scene indices)
+        uint64_t ord = p.wall_order;
+        for (int k = 0; k < p.nW && wm; ++k, ord >>= 4) {
+            const int w = (int)(ord & 15);
+            if (!((wm >> w) & 1)) continue;
+            wm &= ~(1ull << w);
+            wall_exact<EYE>(p.w64[w], w, p, r, h);
+        }
+        return h;
+    }
     while (wm) {
         const int w = __builtin_ctzll(wm);
         wm &= wm - 1;

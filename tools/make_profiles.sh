@@ -14,6 +14,15 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/
     python3 bench.py --steps 200 --warmup 40 --no-cpu-baseline --no-sweep > "$OUT/bench.json" 2> "$OUT/bench.err" \
     || { echo "bench trace failed"; exit 1; }
 echo "bench trace ok"
+# the same bench with one frame at a time (every dispatch serial: rocprof's average is then
+# directly the bench's one-stream kernel_ms) and the driver's default command
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/bench_fif1" -o bench -- \
+    python3 bench.py --steps 200 --warmup 40 --no-cpu-baseline --no-sweep --frames-in-flight 1 \
+    > "$OUT/bench_fif1.json" 2> "$OUT/bench_fif1.err" || { echo "fif1 trace failed"; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/bench_default" -o bench -- \
+    python3 bench.py --steps 20 --warmup 5 > "$OUT/bench_default.json" 2> "$OUT/bench_default.err" \
+    || { echo "default trace failed"; exit 1; }
+echo "fif1 + default traces ok"
 for cfg in $CONFIGS; do
   for prec in $PRECS; do
     for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU"; do

@@ -36,6 +36,11 @@ def main(rnd="r01"):
     bj = os.path.join(src, "bench.json")
     if os.path.exists(bj):
         shutil.copy(bj, os.path.join(dst, "bench_under_rocprof.json"))
+    for run in ("bench_fif1", "bench_default"):  # one-stream bench, the driver's command
+        for f in glob.glob(os.path.join(src, run, "**", "*kernel_stats.csv"), recursive=True):
+            shutil.copy(f, os.path.join(dst, f"{run}_kernel_stats.csv"))
+        if os.path.exists(os.path.join(src, run + ".json")):
+            shutil.copy(os.path.join(src, run + ".json"), os.path.join(dst, f"{run}_under_rocprof.json"))
     sys.path.insert(0, os.path.join(REPO, "ray-tracer-from-scratch_amd"))
     from rtamd import scenes
     traffic_path = os.path.join(REPO, "profiles", "pmc_traffic.json")
