@@ -5,6 +5,9 @@
  * timing events and a staging buffer for host-output renders.  No exception crosses
  * the boundary; every entry point returns an rt_status.
  */
+#ifndef RT_CLUSTER_COS_DEFAULT  // build-time default of RT_OPT_CLUSTER_COS (x 1000)
+#define RT_CLUSTER_COS_DEFAULT 400
+#endif
 #ifndef RT_WALL_ORDER_DEFAULT   // build-time default of RT_OPT_WALL_ORDER (A/B builds)
 #define RT_WALL_ORDER_DEFAULT 0
 #endif
@@ -17,6 +20,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <new>
 #include <vector>
@@ -51,7 +55,9 @@ struct rt_ctx {
         int nS = 0, nW = 0, nP = 0;
         bool int_exp = true;
         size_t off_s64 = 0, off_w32 = 0, off_w64 = 0, off_sj = 0, off_wj = 0, off_mat = 0,
-               off_mat32 = 0, off_wnn = 0, total = 0;
+               off_mat32 = 0, off_wnn = 0, off_clu = 0, off_csph = 0, total = 0;
+        int nclu = 0, clu_axis = 0;  // sphere clusters (rt_device.h), 0 = none
+        float clu_oinf = 0.0f;
         std::vector<char> bytes;    // the device image of the scene (rt_device.h layout)
         std::vector<double> h_sph;  // nS x {cx, cy, cz, radius^2, radius}
         std::vector<double> h_wal;  // nW x {P, n, X, Y, length, width}
@@ -60,6 +66,7 @@ struct rt_ctx {
     unsigned long long* d_stats = nullptr;
     int wave_cull_min = 24;  // spheres from which the wave cull pays (tools/sweep.py)
     bool eye_tables = true;  // RT_OPT_EYE_TABLES
+    float clu_cos = RT_CLUSTER_COS_DEFAULT / 1000.0f;  // RT_OPT_CLUSTER_COS
     bool wall_order = RT_WALL_ORDER_DEFAULT;  // RT_OPT_WALL_ORDER
     bool tile_bins = true;   // RT_OPT_TILE_BINS
     bool row_order = true;   // RT_OPT_ROW_ORDER
@@ -556,6 +563,12 @@ rt::KParams make_params(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, i
     p.mat = reinterpret_cast<const rt::DevMat*>(base + ctx->sc.off_mat);
     p.mat32 = reinterpret_cast<const rt::DevMat32*>(base + ctx->sc.off_mat32);
     p.wnn = reinterpret_cast<const double(*)[4]>(base + ctx->sc.off_wnn);
+    p.clu = reinterpret_cast<const rt::Clu32*>(base + ctx->sc.off_clu);
+    p.csph = reinterpret_cast<const rt::CluSph*>(base + ctx->sc.off_csph);
+    p.nclu = ctx->sc.nclu;
+    p.clu_axis = ctx->sc.clu_axis;
+    p.clu_cos = ctx->clu_cos;
+    p.clu_oinf = ctx->sc.clu_oinf;
     p.nS = ctx->sc.nS;
     p.nW = ctx->sc.nW;
     p.int_exp = ctx->sc.int_exp ? 1 : 0;
@@ -699,7 +712,47 @@ int pack_scene(const rt_prim* prims, int32_t n, rt_ctx::SceneHost& sc) {
     const size_t off_mat = align_up(off_wj + nW * sizeof(int32_t), 256);
     const size_t off_mat32 = align_up(off_mat + (nS + nW) * sizeof(rt::DevMat), 256);
     const size_t off_wnn = align_up(off_mat32 + (nS + nW) * sizeof(rt::DevMat32), 256);
-    const size_t total = align_up(off_wnn + nW * 4 * sizeof(double), 256) + 256;
+    // sphere clusters (rt_device.h): leaves of <= CLU_SIZE spheres from median splits
+    std::vector<std::vector<int>> leaves;
+    int clu_axis = 0;
+    if (nS >= 2 * rt::CLU_SIZE && nS <= (size_t)rt::CLU_SIZE * rt::CLU_MAX / 2) {
+        std::vector<int> all(nS);
+        for (size_t s = 0; s < nS; s++) all[s] = (int)s;
+        bool finite = true;
+        for (const Sph& a : sph)
+            finite = finite && std::isfinite(a.c[0]) && std::isfinite(a.c[1]) &&
+                     std::isfinite(a.c[2]) && std::isfinite(a.r);
+        // median split on the widest axis of the centres until <= CLU_SIZE per leaf
+        std::function<void(std::vector<int>&, bool)> split = [&](std::vector<int>& ids, bool top) {
+            if (ids.size() <= (size_t)rt::CLU_SIZE) {
+                leaves.push_back(ids);
+                return;
+            }
+            double lo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, hi[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+            for (int i : ids)
+                for (int q = 0; q < 3; q++) {
+                    lo[q] = std::min(lo[q], sph[i].c[q]);
+                    hi[q] = std::max(hi[q], sph[i].c[q]);
+                }
+            int ax = 0;
+            for (int q = 1; q < 3; q++)
+                if (hi[q] - lo[q] > hi[ax] - lo[ax]) ax = q;
+            if (top) clu_axis = ax;
+            const size_t mid = ids.size() / 2;
+            std::nth_element(ids.begin(), ids.begin() + mid, ids.end(), [&](int a, int b) {
+                return sph[a].c[ax] < sph[b].c[ax] || (sph[a].c[ax] == sph[b].c[ax] && a < b);
+            });
+            std::vector<int> l(ids.begin(), ids.begin() + mid), r(ids.begin() + mid, ids.end());
+            split(l, false);
+            split(r, false);
+        };
+        if (finite) split(all, true);
+        if (leaves.size() > (size_t)rt::CLU_MAX) leaves.clear();
+    }
+    const size_t nclu = leaves.size();
+    const size_t off_clu = align_up(off_wnn + nW * 4 * sizeof(double), 256);
+    const size_t off_csph = align_up(off_clu + nclu * sizeof(rt::Clu32), 256);
+    const size_t total = align_up(off_csph + nclu * rt::CLU_SIZE * sizeof(rt::CluSph), 256) + 256;
     sc.bytes.assign(total, 0);
     sc.total = total;
     std::vector<char>& host = sc.bytes;
@@ -712,6 +765,8 @@ int pack_scene(const rt_prim* prims, int32_t n, rt_ctx::SceneHost& sc) {
     auto* mat = reinterpret_cast<rt::DevMat*>(host.data() + off_mat);
     auto* mat32 = reinterpret_cast<rt::DevMat32*>(host.data() + off_mat32);
     auto* wnn = reinterpret_cast<double(*)[4]>(host.data() + off_wnn);
+    auto* clu = reinterpret_cast<rt::Clu32*>(host.data() + off_clu);
+    auto* csph = reinterpret_cast<rt::CluSph*>(host.data() + off_csph);
     auto put_mat = [&](size_t slot, const rt_material& m) {
         rt::DevMat& d = mat[slot];
         for (int k = 0; k < 3; k++) d.color[k] = m.color[k];
@@ -739,6 +794,33 @@ int pack_scene(const rt_prim* prims, int32_t n, rt_ctx::SceneHost& sc) {
         d[3] = sph[s].r * sph[s].r;  // scene.cpp:51
         sj[s] = sph[s].j;
         put_mat(s, prims[sph[s].j].mat);
+    }
+    double clu_scale = 1.0;
+    for (size_t c = 0; c < nclu; c++) {
+        double lo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, hi[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+        double scale = 1.0;
+        for (size_t k = 0; k < (size_t)rt::CLU_SIZE; k++) {
+            rt::CluSph& cs = csph[c * rt::CLU_SIZE + k];
+            cs.slot = -1;
+            if (k >= leaves[c].size()) continue;
+            const int si = leaves[c][k];
+            for (int q = 0; q < 4; q++) cs.c[q] = s64[si / 4].v[si % 4][q];
+            cs.slot = si;
+            for (int q = 0; q < 3; q++) {
+                const double rr = std::fabs(sph[si].r);
+                lo[q] = std::min(lo[q], sph[si].c[q] - rr);
+                hi[q] = std::max(hi[q], sph[si].c[q] + rr);
+                scale = std::max(scale, std::fabs(sph[si].c[q]) + rr);
+            }
+        }
+        // margin: far above the fp32 rounding of the box, the ray and the slab arithmetic
+        // (~1e-6 relative), so a ray the exact test finds hitting a ball enters the box
+        const double m = 1e-3 * scale;
+        clu_scale = std::max(clu_scale, scale);
+        for (int q = 0; q < 3; q++) {
+            clu[c].lo[q] = (float)(lo[q] - m);
+            clu[c].hi[q] = (float)(hi[q] + m);
+        }
     }
     for (size_t w = 0; w < nW; w++) {
         const Wal& a = wal[w];
@@ -798,6 +880,13 @@ int pack_scene(const rt_prim* prims, int32_t n, rt_ctx::SceneHost& sc) {
     sc.off_mat = off_mat;
     sc.off_mat32 = off_mat32;
     sc.off_wnn = off_wnn;
+    sc.off_clu = off_clu;
+    sc.off_csph = off_csph;
+    sc.nclu = (int)nclu;
+    sc.clu_axis = clu_axis;
+    // origins up to 100x the scene's extent: fp32 errors of the slab test ~1e-5 x scale,
+    // 100x below the box margin
+    sc.clu_oinf = (float)(100.0 * clu_scale);
     return RT_OK;
 }
 
@@ -996,6 +1085,10 @@ int rt_set_option(rt_ctx* ctx, int32_t option, int64_t value) {
             return RT_OK;
         case RT_OPT_STATS_DEVICE_PTR:
             ctx->d_stats = reinterpret_cast<unsigned long long*>(static_cast<intptr_t>(value));
+            return RT_OK;
+        case RT_OPT_CLUSTER_COS:
+            if (value < -2000 || value > 2000) return RT_ERR_INVALID_ARG;
+            ctx->clu_cos = (float)value / 1000.0f;
             return RT_OK;
         case RT_OPT_WALL_ORDER:
             if (value != 0 && value != 1) return RT_ERR_INVALID_ARG;

@@ -113,6 +113,27 @@ struct PrimBox {
     int16_t x0, x1, i0, i1;  // inclusive pixel box (frame rows); x0 > x1 = never hit
 };
 
+// Sphere clusters for the cull kernels' wide-cone waves (rt_trace.hip clusters_scan).  The
+// host splits the spheres at the median of the centres' widest axis until each leaf holds
+// <= CLU_SIZE of them (rt_capi.cpp build_clusters); each leaf gets an fp32 box around its
+// balls widened by a margin far above fp32 rounding, and a copy of its spheres' exact fp64
+// records in leaf order.  A lane tests its own ray against the leaf boxes, then runs the
+// exact test on the spheres of its own leaves only: a wave's iteration count is its worst
+// lane's, not the union of its lanes' candidates (which is what the wave cone pays when the
+// live rays point everywhere).
+constexpr int CLU_SIZE = 8;
+constexpr int CLU_MAX = 64;
+struct alignas(32) Clu32 {
+    float lo[3], hi[3];
+    float pad[2];
+};
+struct alignas(64) CluSph {
+    double c[4];     // cx, cy, cz, radius^2 (the SphG64 record)
+    int32_t slot;    // material slot = sphere index, -1 = padding
+    int32_t pad[7];
+};
+static_assert(sizeof(Clu32) == 32 && sizeof(CluSph) == 64, "cluster layout");
+
 // Dispatch order given explicitly: up to ROW_PERM_MAX units (tile rows of 8 pixel rows, or
 // parts of them), int16 each, in the kernel arguments.
 #ifndef RT_ROW_PERM_MAX
@@ -162,6 +183,13 @@ struct KParams {
                                         // wall slot, nearest to the camera first (host)
     double eye_s[EYE_MAX_S][4];         // sphere s: {oc.x, oc.y, oc.z, |oc|^2 - r^2}
     double eye_w[EYE_MAX_W];            // wall w: dot(P - pos, n)
+    const Clu32* clu;      // [nclu] sphere-cluster boxes (cull kernels), see above
+    const CluSph* csph;    // [nclu * CLU_SIZE] their spheres in cluster order
+    int32_t nclu;          // 0 = no clusters
+    int32_t clu_axis;      // axis of the first split (0..2): lanes walk clusters against it
+    float clu_cos;         // wide-cone waves (cone cos(half-angle) < clu_cos) use clusters
+    float clu_oinf;        // rays whose |origin|inf exceeds it test every cluster (the box
+                           // margin covers fp32 rounding only for origins near the scene)
 };
 // by-value kernel arguments of up to 16 KB arrive intact (tools/ubench/kernarg_size.hip,
 // kernarg_stale.hip: consistent across back-to-back launches)

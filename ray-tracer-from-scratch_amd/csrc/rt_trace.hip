@@ -82,6 +82,9 @@
 #ifndef RT_BOX_SCHED_BARRIER
 #define RT_BOX_SCHED_BARRIER 1
 #endif
+#ifndef RT_CLUSTERS        // 1: cull kernels' wide-cone waves scan per-lane sphere clusters
+#define RT_CLUSTERS 1
+#endif
 #ifndef RT_WALL_ORDER      // 1: the primary scan visits walls in the host's per-frame order
 #define RT_WALL_ORDER 1    // (nearest to the camera first) when KParams::wall_order is set
 #endif
@@ -1042,7 +1045,54 @@ __device__ __forceinline__ uint64_t mirror_keep(const KParams& p, bool alive, co
 
 /* find_closest_hit for one segment of every live lane: the wave-culled scan (CULL) or the
  * linear scan.  Converged: every lane of the wave calls it (alive masks the tests). */
-template <bool MIXED, bool CULL>
+/* Sphere clusters (rt_device.h Clu32/CluSph): a wide-cone wave's lanes each test their own
+ * ray against the cluster boxes, then walk their own clusters — against the first split's
+ * axis along the ray, so roughly near to far — skipping a cluster whose box entry already
+ * lies beyond the lane's best hit, and run the exact test (order-independent tie rule) on
+ * its spheres.  Conservative: the boxes are the balls' bounds widened by 1e-3 x the scene
+ * extent, against fp32 slab errors ~1e-5 x extent for origins within 100 x the extent
+ * (others test every cluster, unpruned); a skipped cluster's spheres lie at a world
+ * distance >= t_entry |d| > best, so they lose even a tie.  slab_t: entry parameter of the
+ * ray into the box (0 inside), +inf on a miss; NaN slab terms (origin on a box plane with
+ * d = 0 there: the ray misses the ball by the margin) reject. */
+__device__ __forceinline__ float slab_t(const Clu32& B, const f3 o, const f3 inv) {
+    const float x1 = (B.lo[0] - o.x) * inv.x, x2 = (B.hi[0] - o.x) * inv.x;
+    const float y1 = (B.lo[1] - o.y) * inv.y, y2 = (B.hi[1] - o.y) * inv.y;
+    const float z1 = (B.lo[2] - o.z) * inv.z, z2 = (B.hi[2] - o.z) * inv.z;
+    const float tn = fmaxf(fmaxf(fminf(x1, x2), fminf(y1, y2)), fmaxf(fminf(z1, z2), 0.0f));
+    const float tf = fminf(fminf(fmaxf(x1, x2), fmaxf(y1, y2)), fmaxf(z1, z2));
+    return tn <= tf ? tn : __builtin_inff();
+}
+__device__ __forceinline__ void clusters_scan(const KParams& p, const RayD& r, bool alive, HitD& h) {
+    const f3 o = F3((float)r.o.x, (float)r.o.y, (float)r.o.z);
+    const f3 d = F3((float)r.d.x, (float)r.d.y, (float)r.d.z);
+    const f3 inv = F3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const bool near = fmax3abs(o.x, o.y, o.z) <= p.clu_oinf;
+    uint64_t cm = 0;
+    for (int c = 0; c < p.nclu; ++c) {  // wave-uniform: scalar loads of the box
+        const bool in = !near || slab_t(p.clu[c], o, inv) < __builtin_inff();
+        cm |= (uint64_t)(alive && in) << c;
+    }
+    const float dax = p.clu_axis == 0 ? d.x : (p.clu_axis == 1 ? d.y : d.z);
+    const bool rev = dax < 0.0f;
+    while (__any(cm != 0)) {
+        if (cm != 0) {
+            const int c = rev ? 63 - __builtin_clzll(cm) : __builtin_ctzll(cm);
+            cm &= ~(1ull << c);
+            const float t = near ? slab_t(p.clu[c], o, inv) : 0.0f;
+            if ((double)t * r.dlen * (1.0 - 1e-3) <= h.dist) {
+                const CluSph* cs = p.csph + c * CLU_SIZE;
+#pragma unroll
+                for (int k = 0; k < CLU_SIZE; ++k) {
+                    const int s = cs[k].slot;
+                    if (s >= 0) sphere_exact<false>(cs[k].c, s, r, h, &p);
+                }
+            }
+        }
+    }
+}
+
+template <bool MIXED, bool CULL, bool CLU>
 __device__ __forceinline__ HitD scan_d(const KParams& p, const RayD& r, bool alive,
                                        bool primary, bool binned, uint64_t keep) {
     HitD h = no_hit();
@@ -1053,7 +1103,12 @@ __device__ __forceinline__ HitD scan_d(const KParams& p, const RayD& r, bool ali
         if (RT_WALLS_FIRST && alive) walls_d<MIXED>(p, r, rf, h);
         const Cone cn = wave_cone(F3((float)r.o.x, (float)r.o.y, (float)r.o.z),
                                   F3((float)r.d.x, (float)r.d.y, (float)r.d.z), alive);
-        for (int c0 = 0; c0 < p.nS; c0 += 64) {
+        // a wide cone (live rays pointing everywhere) culls little: each lane its own clusters
+        // (PATH64 only: in the fp64-colour kernels the extra code costs more than it saves,
+        // A/B c3 F64 +40%)
+        const bool clusters = RT_CLUSTERS && CLU && p.nclu > 0 && cn.cos_t < p.clu_cos;
+        if (clusters) clusters_scan(p, r, alive, h);
+        for (int c0 = 0; !clusters && c0 < p.nS; c0 += 64) {
             float lb;
             SphRec rec;
             uint64_t m = cull_chunk<true>(p, cn, c0, &lb, rec);
@@ -1160,7 +1215,7 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
             else DIAG(14);
         }
 #endif
-        const HitD h = scan_d<MIXED, CULL>(p, r, alive, k == 0, km != ~0ull, km);
+        const HitD h = scan_d<MIXED, CULL, !COLOR64>(p, r, alive, k == 0, km != ~0ull, km);
         if (k == 0) STAGE(2);
         const bool last = k >= p.depth || k >= MAXD;  // remaining_iterations <= 0 (main.cpp:105)
         if (LAZY && !terms && __any(alive && !last && h.slot >= 0)) {  // a reflection follows

@@ -55,6 +55,7 @@ RT_OPT_ROW_FEEDBACK = 8
 RT_OPT_PIXEL_PAIRS = 9
 RT_OPT_ROW_FEEDBACK_WARM = 10
 RT_OPT_WALL_ORDER = 11
+RT_OPT_CLUSTER_COS = 12
 
 
 class rt_material(C.Structure):

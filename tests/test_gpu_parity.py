@@ -439,6 +439,44 @@ def test_wave_cull_is_output_invariant(rend, prec):
         rend.set_option(capi.RT_OPT_WAVE_CULL_MIN_SPHERES, 24)
 
 
+@pytest.mark.parametrize("prec", [capi.RT_PREC_F64, capi.RT_PREC_MIXED, capi.RT_PREC_PATH64])
+def test_sphere_clusters_are_output_invariant(rend, prec):
+    """RT_OPT_CLUSTER_COS: wide-cone waves of the cull kernels test each lane's ray against
+    sphere clusters (rt_device.h Clu32) and run the exact test on its own clusters only,
+    pruning clusters beyond the lane's best hit.  Forced on for every wave (2000), off
+    (-2000) and at the default, frames are bitwise those of the linear scan — with
+    duplicated spheres (exact ties across clusters: the lower scene index must win), cameras
+    inside the sphere cloud and far outside it (origins past the box margin's range test
+    every cluster unpruned), deep bounces."""
+    rng = np.random.default_rng(23)
+    try:
+        for trial, ns in enumerate((24, 70, 129, 256)):
+            sc = scenes.synthetic_scene(ns, int(rng.integers(0, 7)),
+                                        seed=int(rng.integers(1 << 30)))
+            sph = [o for o in sc if o.kind == capi.RT_PRIM_SPHERE]
+            for k in range(3):  # copies of earlier spheres, another colour, later in order
+                o = sph[int(rng.integers(len(sph)))]
+                sc.append(scenes.Sphere(scenes.Material(tuple(rng.uniform(0, 1, 3)), .6),
+                                        o.position, o.radius))
+            rend.set_scene(scenes.to_prims(sc))
+            far = trial == 3
+            pos = (np.array([-400.0, 30.0, 10.0]) if far else rng.uniform([2, -3, -1], [8, 3, 2]))
+            look = np.array([5.0, 0.0, 0.5]) if far else pos + rng.normal(size=3)
+            cam = capi.camera_init(pos, look, (0, 0, -1), 2.0 if far else 100.0, 16 / 9, 160.0)
+            depth = 8
+            rend.set_option(capi.RT_OPT_WAVE_CULL_MIN_SPHERES, 2**31 - 1)
+            ref, rst = rend.render(cam, depth, prec, 0, capi.RT_OUT_RGB_F64, count_segments=True)
+            rend.set_option(capi.RT_OPT_WAVE_CULL_MIN_SPHERES, 0)
+            for cc in (2000, -2000, 400):
+                rend.set_option(capi.RT_OPT_CLUSTER_COS, cc)
+                img, st = rend.render(cam, depth, prec, 0, capi.RT_OUT_RGB_F64, count_segments=True)
+                assert st.segments == rst.segments, (trial, cc)
+                assert np.array_equal(img.view(np.uint64), ref.view(np.uint64)), (trial, cc)
+    finally:
+        rend.set_option(capi.RT_OPT_CLUSTER_COS, 400)
+        rend.set_option(capi.RT_OPT_WAVE_CULL_MIN_SPHERES, 24)
+
+
 # ---------------------------------------------------------------- eye tables
 @pytest.mark.parametrize("prec", [capi.RT_PREC_F64, capi.RT_PREC_MIXED, capi.RT_PREC_PATH64])
 def test_eye_tables_are_output_invariant(rend, prec):
