@@ -715,7 +715,7 @@ int pack_scene(const rt_prim* prims, int32_t n, rt_ctx::SceneHost& sc) {
     // sphere clusters (rt_device.h): leaves of <= CLU_SIZE spheres from median splits
     std::vector<std::vector<int>> leaves;
     int clu_axis = 0;
-    if (nS >= 2 * rt::CLU_SIZE && nS <= (size_t)rt::CLU_SIZE * rt::CLU_MAX / 2) {
+    if (nS >= 2 * rt::CLU_SIZE && nS <= (size_t)rt::CLU_SIZE * rt::CLU_MAX) {
         std::vector<int> all(nS);
         for (size_t s = 0; s < nS; s++) all[s] = (int)s;
         bool finite = true;

@@ -121,7 +121,10 @@ struct PrimBox {
 // exact test on the spheres of its own leaves only: a wave's iteration count is its worst
 // lane's, not the union of its lanes' candidates (which is what the wave cone pays when the
 // live rays point everywhere).
-constexpr int CLU_SIZE = 8;
+#ifndef RT_CLU_SIZE
+#define RT_CLU_SIZE 8
+#endif
+constexpr int CLU_SIZE = RT_CLU_SIZE;
 constexpr int CLU_MAX = 64;
 struct alignas(32) Clu32 {
     float lo[3], hi[3];

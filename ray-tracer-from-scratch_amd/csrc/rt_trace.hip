@@ -136,7 +136,7 @@ __device__ unsigned long long g_diag[16];
     } while (0)
 #endif
 #ifndef RT_WPE_PATH64           // occupancy targets (waves_per_eu below), A/B knobs
-#define RT_WPE_PATH64 4
+#define RT_WPE_PATH64 5
 #endif
 #ifndef RT_WPE_PATH64_LIN_BONUS
 #define RT_WPE_PATH64_LIN_BONUS 0
@@ -2018,7 +2018,9 @@ constexpr int waves_per_eu() {
     if (PREC == PREC_F32)
         w = 5 + RT_WPE_F32_BONUS - (tier > 0 ? 1 : 0) - ((SUN && tier == 2) ? 1 : 0);
     else if (PREC == PREC_PATH64)
-        w = RT_WPE_PATH64 - (tier == 2 ? 1 : 0) - ((SUN && tier > 0) ? 1 : 0) +
+        // (5 waves: A/B c5 -7%, c3 -5% with 20 B of spills in the cull kernels; the sun
+        // variants, whose spills would be 56-96 B, keep 4)
+        w = RT_WPE_PATH64 - (tier == 2 ? 1 : 0) - (SUN ? 1 : 0) +
             ((!CULL && !SUN && tier == 0) ? RT_WPE_PATH64_LIN_BONUS : 0);
     else
         w = (INT_EXP ? (SUN ? 3 : 4) : (SUN ? 2 : 3)) - (tier > 0 ? 1 : 0) -
