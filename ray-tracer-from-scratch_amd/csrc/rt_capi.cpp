@@ -805,6 +805,7 @@ int pack_scene(const rt_prim* prims, int32_t n, rt_ctx::SceneHost& sc) {
             if (k >= leaves[c].size()) continue;
             const int si = leaves[c][k];
             for (int q = 0; q < 4; q++) cs.c[q] = s64[si / 4].v[si % 4][q];
+            for (int q = 0; q < 4; q++) cs.f[q] = s32[si / 4].c[q][si % 4];
             cs.slot = si;
             for (int q = 0; q < 3; q++) {
                 const double rr = std::fabs(sph[si].r);

@@ -132,8 +132,9 @@ struct alignas(32) Clu32 {
 };
 struct alignas(64) CluSph {
     double c[4];     // cx, cy, cz, radius^2 (the SphG64 record)
+    float f[4];      // cx, cy, cz, radius (the SphG32 record, F32 kernels)
     int32_t slot;    // material slot = sphere index, -1 = padding
-    int32_t pad[7];
+    int32_t pad[3];
 };
 static_assert(sizeof(Clu32) == 32 && sizeof(CluSph) == 64, "cluster layout");
 

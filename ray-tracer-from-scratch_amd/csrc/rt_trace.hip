@@ -85,6 +85,9 @@
 #ifndef RT_CLUSTERS        // 1: cull kernels' wide-cone waves scan per-lane sphere clusters
 #define RT_CLUSTERS 1
 #endif
+#ifndef RT_CLUSTERS_F32    // 1: the same for the F32 cull kernels
+#define RT_CLUSTERS_F32 1
+#endif
 #ifndef RT_WALL_ORDER      // 1: the primary scan visits walls in the host's per-frame order
 #define RT_WALL_ORDER 1    // (nearest to the camera first) when KParams::wall_order is set
 #endif
@@ -1700,6 +1703,39 @@ __device__ __forceinline__ void sphere_f(const float* S, int s, f3 o, f3 d, floa
     }
 }
 
+/* clusters_scan for the F32 kernels: the same walk over the lane's own clusters with the
+ * fp32 sphere test (sphere_f, scene-index tie rule); a pruned cluster's spheres lie at a
+ * distance >= t_entry |d| > best (box margin 1e-3 x the scene extent). */
+__device__ __forceinline__ void clusters_scan_f(const KParams& p, f3 o, f3 d, float a, float ra,
+                                                float rl, bool alive, float& best, float& bpt,
+                                                int& slot) {
+    const f3 inv = F3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const bool near = fmax3abs(o.x, o.y, o.z) <= p.clu_oinf;
+    uint64_t cm = 0;
+    for (int c = 0; c < p.nclu; ++c) {
+        const bool in = !near || slab_t(p.clu[c], o, inv) < __builtin_inff();
+        cm |= (uint64_t)(alive && in) << c;
+    }
+    const float dax = p.clu_axis == 0 ? d.x : (p.clu_axis == 1 ? d.y : d.z);
+    const bool rev = dax < 0.0f;
+    const float dl = a * rl;  // |d|
+    while (__any(cm != 0)) {
+        if (cm != 0) {
+            const int c = rev ? 63 - __builtin_clzll(cm) : __builtin_ctzll(cm);
+            cm &= ~(1ull << c);
+            const float t = near ? slab_t(p.clu[c], o, inv) : 0.0f;
+            if (t * dl * (1.0f - 1e-3f) <= best) {
+                const CluSph* cs = p.csph + c * CLU_SIZE;
+#pragma unroll
+                for (int k = 0; k < CLU_SIZE; ++k) {
+                    const int s = cs[k].slot;
+                    if (s >= 0) sphere_f<false>(cs[k].f, s, o, d, a, ra, rl, best, bpt, slot, &p);
+                }
+            }
+        }
+    }
+}
+
 /* Two spheres (k0, k0+1 of group G) per packed fp32 instruction: the cheap prefix
  * (oc, b/2, c, det) runs as v_pk_* on {sphere k0, sphere k0+1}; the rare hit path
  * (sqrt, divide, compare) per sphere.  Same arithmetic as sphere_f, lane for lane. */
@@ -1825,7 +1861,10 @@ __device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, bool
         } else if (CULL) {
             if (RT_WALLS_FIRST && alive) walls_f(p, o, d, best, slot);
             const Cone cn = wave_cone(o, d, alive);
-            for (int c0 = 0; c0 < p.nS; c0 += 64) {
+            // wide cone: each lane its own sphere clusters (clusters_scan)
+            const bool clusters = RT_CLUSTERS_F32 && p.nclu > 0 && cn.cos_t < p.clu_cos;
+            if (clusters) clusters_scan_f(p, o, d, a, ra, rl, alive, best, bpt, slot);
+            for (int c0 = 0; !clusters && c0 < p.nS; c0 += 64) {
                 float lb;
                 SphRec rec;
                 uint64_t m = cull_chunk<false>(p, cn, c0, &lb, rec);
@@ -2016,7 +2055,9 @@ constexpr int waves_per_eu() {
     int w = 0;
     if (PREC == PREC_F64 && !CULL && !SUN && tier == 0) return 4 + RT_WPE_F64_LIN_BONUS;
     if (PREC == PREC_F32)
-        w = 5 + RT_WPE_F32_BONUS - (tier > 0 ? 1 : 0) - ((SUN && tier == 2) ? 1 : 0);
+        // (cull kernels one wave more since the sphere clusters: A/B c5 -4%, c3 -1% vs 5)
+        w = 5 + RT_WPE_F32_BONUS - (tier > 0 ? 1 : 0) - ((SUN && tier == 2) ? 1 : 0) +
+            ((CULL && !SUN && tier == 0) ? 1 : 0);
     else if (PREC == PREC_PATH64)
         // (5 waves: A/B c5 -7%, c3 -5% with 20 B of spills in the cull kernels; the sun
         // variants, whose spills would be 56-96 B, keep 4)

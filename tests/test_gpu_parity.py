@@ -439,7 +439,8 @@ def test_wave_cull_is_output_invariant(rend, prec):
         rend.set_option(capi.RT_OPT_WAVE_CULL_MIN_SPHERES, 24)
 
 
-@pytest.mark.parametrize("prec", [capi.RT_PREC_F64, capi.RT_PREC_MIXED, capi.RT_PREC_PATH64])
+@pytest.mark.parametrize("prec", [capi.RT_PREC_F64, capi.RT_PREC_MIXED, capi.RT_PREC_PATH64,
+                                  capi.RT_PREC_F32])
 def test_sphere_clusters_are_output_invariant(rend, prec):
     """RT_OPT_CLUSTER_COS: wide-cone waves of the cull kernels test each lane's ray against
     sphere clusters (rt_device.h Clu32) and run the exact test on its own clusters only,
