@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -55,7 +56,7 @@ struct rt_ctx {
         int nS = 0, nW = 0, nP = 0;
         bool int_exp = true;
         size_t off_s64 = 0, off_w32 = 0, off_w64 = 0, off_sj = 0, off_wj = 0, off_mat = 0,
-               off_mat32 = 0, off_wnn = 0, off_clu = 0, off_csph = 0, total = 0;
+               off_mat32 = 0, off_wnn = 0, off_clu = 0, off_csph = 0, off_cord = 0, total = 0;
         int nclu = 0, clu_axis = 0;  // sphere clusters (rt_device.h), 0 = none
         float clu_oinf = 0.0f;
         std::vector<char> bytes;    // the device image of the scene (rt_device.h layout)
@@ -565,6 +566,7 @@ rt::KParams make_params(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, i
     p.wnn = reinterpret_cast<const double(*)[4]>(base + ctx->sc.off_wnn);
     p.clu = reinterpret_cast<const rt::Clu32*>(base + ctx->sc.off_clu);
     p.csph = reinterpret_cast<const rt::CluSph*>(base + ctx->sc.off_csph);
+    p.cord = reinterpret_cast<const uint8_t*>(base + ctx->sc.off_cord);
     p.nclu = ctx->sc.nclu;
     p.clu_axis = ctx->sc.clu_axis;
     p.clu_cos = ctx->clu_cos;
@@ -752,7 +754,8 @@ int pack_scene(const rt_prim* prims, int32_t n, rt_ctx::SceneHost& sc) {
     const size_t nclu = leaves.size();
     const size_t off_clu = align_up(off_wnn + nW * 4 * sizeof(double), 256);
     const size_t off_csph = align_up(off_clu + nclu * sizeof(rt::Clu32), 256);
-    const size_t total = align_up(off_csph + nclu * rt::CLU_SIZE * sizeof(rt::CluSph), 256) + 256;
+    const size_t off_cord = align_up(off_csph + nclu * rt::CLU_SIZE * sizeof(rt::CluSph), 256);
+    const size_t total = align_up(off_cord + 8 * rt::CLU_MAX, 256) + 256;
     sc.bytes.assign(total, 0);
     sc.total = total;
     std::vector<char>& host = sc.bytes;
@@ -796,6 +799,7 @@ int pack_scene(const rt_prim* prims, int32_t n, rt_ctx::SceneHost& sc) {
         put_mat(s, prims[sph[s].j].mat);
     }
     double clu_scale = 1.0;
+    std::vector<std::array<double, 3>> cen(nclu);
     for (size_t c = 0; c < nclu; c++) {
         double lo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, hi[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
         double scale = 1.0;
@@ -818,6 +822,7 @@ int pack_scene(const rt_prim* prims, int32_t n, rt_ctx::SceneHost& sc) {
         // (~1e-6 relative), so a ray the exact test finds hitting a ball enters the box
         const double m = 1e-3 * scale;
         clu_scale = std::max(clu_scale, scale);
+        for (int q = 0; q < 3; q++) cen[c][q] = 0.5 * (lo[q] + hi[q]);
         for (int q = 0; q < 3; q++) {
             clu[c].lo[q] = (float)(lo[q] - m);
             clu[c].hi[q] = (float)(hi[q] + m);
@@ -880,6 +885,23 @@ int pack_scene(const rt_prim* prims, int32_t n, rt_ctx::SceneHost& sc) {
     sc.off_wj = off_wj;
     sc.off_mat = off_mat;
     sc.off_mat32 = off_mat32;
+    // near-to-far cluster order per direction octant: by the box centre along the octant's
+    // diagonal (any order is exact; this one lets the lanes' pruning start from near hits)
+    auto* cord = reinterpret_cast<uint8_t*>(host.data() + off_cord);
+    for (int o = 0; o < 8 && nclu > 0; o++) {
+        const double sx = (o & 1) ? -1.0 : 1.0, sy = (o & 2) ? -1.0 : 1.0, sz = (o & 4) ? -1.0 : 1.0;
+        std::vector<int> ord(nclu);
+        for (size_t c = 0; c < nclu; c++) ord[c] = (int)c;
+        std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) {
+            return sx * cen[a][0] + sy * cen[a][1] + sz * cen[a][2] <
+                   sx * cen[b][0] + sy * cen[b][1] + sz * cen[b][2];
+        });
+        for (size_t k = 0; k < nclu; k++) {
+            cord[o * rt::CLU_MAX + k] = (uint8_t)ord[k];
+            clu[ord[k]].rank[o] = (uint8_t)k;
+        }
+    }
+    sc.off_cord = off_cord;
     sc.off_wnn = off_wnn;
     sc.off_clu = off_clu;
     sc.off_csph = off_csph;

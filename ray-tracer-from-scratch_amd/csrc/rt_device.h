@@ -128,7 +128,9 @@ constexpr int CLU_SIZE = RT_CLU_SIZE;
 constexpr int CLU_MAX = 64;
 struct alignas(32) Clu32 {
     float lo[3], hi[3];
-    float pad[2];
+    uint8_t rank[8];  // position of this cluster in the near-to-far order of each direction
+                      // octant (bit 0/1/2 = d.x/d.y/d.z < 0): the host sorts the clusters by
+                      // their centroid along the octant's diagonal
 };
 struct alignas(64) CluSph {
     double c[4];     // cx, cy, cz, radius^2 (the SphG64 record)
@@ -189,6 +191,7 @@ struct KParams {
     double eye_w[EYE_MAX_W];            // wall w: dot(P - pos, n)
     const Clu32* clu;      // [nclu] sphere-cluster boxes (cull kernels), see above
     const CluSph* csph;    // [nclu * CLU_SIZE] their spheres in cluster order
+    const uint8_t* cord;   // [8][CLU_MAX] cluster at each rank of each octant's order
     int32_t nclu;          // 0 = no clusters
     int32_t clu_axis;      // axis of the first split (0..2): lanes walk clusters against it
     float clu_cos;         // wide-cone waves (cone cos(half-angle) < clu_cos) use clusters

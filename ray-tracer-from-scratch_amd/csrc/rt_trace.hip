@@ -85,6 +85,12 @@
 #ifndef RT_CLUSTERS        // 1: cull kernels' wide-cone waves scan per-lane sphere clusters
 #define RT_CLUSTERS 1
 #endif
+#ifndef RT_CLU_OCT         // 1: lanes walk their clusters in a per-octant near-to-far order
+#define RT_CLU_OCT 1
+#endif
+#ifndef RT_CLU_OCT_F32     // the same for the F32 kernels (A/B: c5 F32 +4.5%, PATH64 -2..2.5%)
+#define RT_CLU_OCT_F32 0
+#endif
 #ifndef RT_CLUSTERS_F32    // 1: the same for the F32 cull kernels
 #define RT_CLUSTERS_F32 1
 #endif
@@ -1058,6 +1064,19 @@ __device__ __forceinline__ uint64_t mirror_keep(const KParams& p, bool alive, co
  * distance >= t_entry |d| > best, so they lose even a tie.  slab_t: entry parameter of the
  * ray into the box (0 inside), +inf on a miss; NaN slab terms (origin on a box plane with
  * d = 0 there: the ray misses the ball by the margin) reject. */
+/* RT_CLU_OCT: the lane walks its clusters near to far in the host's order for its
+ * direction octant (Clu32::rank, KParams::cord); otherwise in index order, reversed when
+ * the ray runs against the first split's axis. */
+__device__ __forceinline__ int clu_octant(const f3 d) {
+    return (d.x < 0.0f ? 1 : 0) | (d.y < 0.0f ? 2 : 0) | (d.z < 0.0f ? 4 : 0);
+}
+template <bool OCT>
+__device__ __forceinline__ int clu_bit(const Clu32& B, int oct, int c) {
+    if (!OCT) return c;
+    const uint32_t lo = *reinterpret_cast<const uint32_t*>(B.rank);
+    const uint32_t hi = *reinterpret_cast<const uint32_t*>(B.rank + 4);
+    return (int)(((oct < 4 ? lo : hi) >> (8 * (oct & 3))) & 0xff);
+}
 __device__ __forceinline__ float slab_t(const Clu32& B, const f3 o, const f3 inv) {
     const float x1 = (B.lo[0] - o.x) * inv.x, x2 = (B.hi[0] - o.x) * inv.x;
     const float y1 = (B.lo[1] - o.y) * inv.y, y2 = (B.hi[1] - o.y) * inv.y;
@@ -1071,17 +1090,19 @@ __device__ __forceinline__ void clusters_scan(const KParams& p, const RayD& r, b
     const f3 d = F3((float)r.d.x, (float)r.d.y, (float)r.d.z);
     const f3 inv = F3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     const bool near = fmax3abs(o.x, o.y, o.z) <= p.clu_oinf;
-    uint64_t cm = 0;
+    const int oct = clu_octant(d);
+    uint64_t cm = 0;  // bit k: the cluster at rank k of this lane's octant order
     for (int c = 0; c < p.nclu; ++c) {  // wave-uniform: scalar loads of the box
         const bool in = !near || slab_t(p.clu[c], o, inv) < __builtin_inff();
-        cm |= (uint64_t)(alive && in) << c;
+        cm |= (uint64_t)(alive && in) << clu_bit<RT_CLU_OCT>(p.clu[c], oct, c);
     }
     const float dax = p.clu_axis == 0 ? d.x : (p.clu_axis == 1 ? d.y : d.z);
-    const bool rev = dax < 0.0f;
+    const bool rev = !RT_CLU_OCT && dax < 0.0f;
     while (__any(cm != 0)) {
         if (cm != 0) {
-            const int c = rev ? 63 - __builtin_clzll(cm) : __builtin_ctzll(cm);
-            cm &= ~(1ull << c);
+            const int k = rev ? 63 - __builtin_clzll(cm) : __builtin_ctzll(cm);
+            cm &= ~(1ull << k);
+            const int c = RT_CLU_OCT ? (int)p.cord[oct * CLU_MAX + k] : k;
             const float t = near ? slab_t(p.clu[c], o, inv) : 0.0f;
             if ((double)t * r.dlen * (1.0 - 1e-3) <= h.dist) {
                 const CluSph* cs = p.csph + c * CLU_SIZE;
@@ -1711,18 +1732,20 @@ __device__ __forceinline__ void clusters_scan_f(const KParams& p, f3 o, f3 d, fl
                                                 int& slot) {
     const f3 inv = F3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     const bool near = fmax3abs(o.x, o.y, o.z) <= p.clu_oinf;
+    const int oct = clu_octant(d);
     uint64_t cm = 0;
     for (int c = 0; c < p.nclu; ++c) {
         const bool in = !near || slab_t(p.clu[c], o, inv) < __builtin_inff();
-        cm |= (uint64_t)(alive && in) << c;
+        cm |= (uint64_t)(alive && in) << clu_bit<RT_CLU_OCT_F32>(p.clu[c], oct, c);
     }
     const float dax = p.clu_axis == 0 ? d.x : (p.clu_axis == 1 ? d.y : d.z);
-    const bool rev = dax < 0.0f;
+    const bool rev = !RT_CLU_OCT_F32 && dax < 0.0f;
     const float dl = a * rl;  // |d|
     while (__any(cm != 0)) {
         if (cm != 0) {
-            const int c = rev ? 63 - __builtin_clzll(cm) : __builtin_ctzll(cm);
-            cm &= ~(1ull << c);
+            const int k = rev ? 63 - __builtin_clzll(cm) : __builtin_ctzll(cm);
+            cm &= ~(1ull << k);
+            const int c = RT_CLU_OCT_F32 ? (int)p.cord[oct * CLU_MAX + k] : k;
             const float t = near ? slab_t(p.clu[c], o, inv) : 0.0f;
             if (t * dl * (1.0f - 1e-3f) <= best) {
                 const CluSph* cs = p.csph + c * CLU_SIZE;
