@@ -1,29 +1,30 @@
 #!/usr/bin/env python3
 """bench.py — Mrays/s + ms/frame of the MI355X trace/shade path (BASELINE.json metric).
 
-A "step" is one pass of the hot path over one batch of synthetic input: every rank
-renders one full frame of the configured scene (default c2: 1920x1080, 8 spheres +
-4 walls, reflection depth 4) into HBM through the C-ABI (rt_render_device), the scene
-already resident on the device.  With N ranks the batch is N frames of a camera
-fly-through (rank r renders frame r: the camera moved r steps forward the way
-Camera::forward moves it, scene.cpp:121) — frames are independent units, sharded with
-no data-path collective, so `scaling` is "weak".  Consecutive frames of a rank go to
-`--frames-in-flight` output buffers on as many streams (default 2, a double-buffered frame
-loop): every frame is rendered in full, and one frame's last (heaviest) waves overlap the
-next frame's first instead of leaving the GPU draining between launches; `kernel_ms` is
-the one-frame-at-a-time kernel duration.  `--mode tiled` instead splits ONE
-frame into row bands across ranks and gathers them to rank 0 (RCCL), the strong-scaling
-layout of BASELINE config 4.
+A "step" is one frame of the hot path over synthetic input: the configured scene (default
+c2: 1920x1080, 8 spheres + 4 walls, reflection depth 4) rendered in full into HBM through
+the C-ABI, the scene already resident on the device.
+
+Default mode `tiled` (BASELINE configs 2 and 4): ONE frame per step split into contiguous
+row bands across the N ranks (one process per GPU), each band rendered by its rank, and the
+bands gathered into rank 0's frame buffer with RCCL send/recv inside the C-ABI's multi-GPU
+frame operator (rt_multi_*, csrc/rt_multi.cpp) — `scaling` "strong" (total work fixed).  At
+N = 1 the one band is the whole frame, rendered in place (no gather).  Consecutive frames go
+to `--frames-in-flight` frame buffers on as many streams (default 2): every frame is
+rendered and gathered in full, and frame k+1's render overlaps frame k's tail and gather.
+With N > 1 the bench also reports, as a side field (`frame_sharded`), the weak layout: N
+independent frames of a camera fly-through per step, no collective.  `--mode frames` makes
+that the headline instead.
 
 Rays = segments = closest-hit queries (primary + reflection), counted exactly by the
 kernel in an untimed census launch.
 
-Order of a run: census; the side measurements (per-precision sweep, sun extension, moving
-camera — before the timed region, so it starts on a GPU at its running clock rather than
-on the ramp out of idle); W warmup steps; K timed steps; the one-stream kernel time.  The
-warmup and timed steps of frames mode are enqueued by one rt_render_device_frames call
-each (every frame's own host work and launch, as a C++ frame loop over rt_render_device
-would do them, without Python's per-call overhead).
+Order of a run: census; side measurements (per-precision kernel sweep, sun-on frame loop,
+moving-camera frame loop — before the timed region, so it starts on a GPU at its running
+clock); W warmup + K timed steps, each enqueued by one C-ABI call per region
+(rt_multi_render_device_frames / rt_render_device_frames: every frame's own host work and
+launch, as a C++ frame loop does them, without Python's per-call overhead); the one-stream
+kernel time; the frame-sharded side run (N > 1); the CPU baseline (rank 0, N = 1).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2] [--precision mixed]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
@@ -63,45 +64,64 @@ def scene_bytes(n_sph: int, n_wall: int, n_prim: int) -> int:
     return 64 * n_sph + 176 * n_wall + 64 * n_prim   # DevSphere / DevWall / DevMat records
 
 
+def cpu_threads() -> dict:
+    """The host's threads as the CPU baseline sees them (OMP_NUM_THREADS =
+    nproc).  On a shared GPU box OMP_NUM_THREADS is this job's CPU share, and the machine's
+    full core count (nproc) is not ours to use, so OMP_NUM_THREADS wins when it is set."""
+    affinity = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    threads = int(omp) if omp and omp.isdigit() and int(omp) > 0 else affinity
+    return {"threads": threads, "nproc": os.cpu_count(), "affinity": affinity,
+            "OMP_NUM_THREADS": omp}
+
+
 def cpu_baseline(cfg, prims, cam, depth, flags, budget_s: float):
     """The oracle's OpenMP restatement (the 'OpenMP CPU path') on this host's cores, on a
-    bounded sample of the same frame: a centred band of rows sized to ~budget_s."""
+    bounded sample of the same frame: a centred band of rows sized to ~budget_s / 3, timed
+    three times, best of 3."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as orc_mod   # test infrastructure: the timed CPU baseline leg only
     orc = orc_mod.Oracle()
-    cores = max(1, min(16, len(os.sched_getaffinity(0))))
+    th = cpu_threads()
+    cores = th["threads"]
     H = cam.height
     probe = min(H, 16)
     r0 = max(0, H // 2 - probe // 2)
     t = time.perf_counter()
     orc.render(prims, cam, depth, flags, row0=r0, nrows=probe, nthreads=cores, want64=False)
     per_row = max(1e-6, (time.perf_counter() - t) / probe)
-    rows = int(min(H, max(probe, budget_s / per_row)))
+    rows = int(min(H, max(probe, budget_s / 3 / per_row)))
     r0 = max(0, H // 2 - rows // 2)
-    # repeat the band until the budget is spent (small frames finish in milliseconds)
-    segs, dt, reps = 0, 0.0, 0
-    while reps == 0 or (dt < budget_s and reps < 10000):
-        t = time.perf_counter()
-        _, _, s = orc.render(prims, cam, depth, flags, row0=r0, nrows=rows, nthreads=cores,
-                             want64=False)
-        dt += time.perf_counter() - t
-        segs += s
-        reps += 1
-    return {"value": round(segs / dt / 1e6, 3), "unit": "Mrays/s", "cores": cores, "kind": "port",
-            "sample": f"{reps} x rows {r0}..{r0 + rows - 1} of the same {cam.width}x{H} frame "
-                      f"({rows * cam.width} px, {segs} segments in {dt:.2f} s), fp64 oracle "
-                      f"restatement (-O2, no FMA), OpenMP schedule(dynamic,1) over rows",
-            "ms_per_frame": round(dt / reps / rows * H * 1e3, 2)}
+    runs = []
+    for _ in range(3):
+        # repeat the band until a third of the budget is spent (small frames take ms)
+        segs, dt, reps = 0, 0.0, 0
+        while reps == 0 or (dt < budget_s / 3 and reps < 10000):
+            t = time.perf_counter()
+            _, _, s = orc.render(prims, cam, depth, flags, row0=r0, nrows=rows, nthreads=cores,
+                                 want64=False)
+            dt += time.perf_counter() - t
+            segs += s
+            reps += 1
+        runs.append((segs / dt, dt / reps, reps, segs, dt))
+    best = max(runs)
+    return {"value": round(best[0] / 1e6, 3), "unit": "Mrays/s", "cores": cores, "kind": "port",
+            "threads": th,
+            "sample": f"best of 3 runs, each {best[2]} x rows {r0}..{r0 + rows - 1} of the same "
+                      f"{cam.width}x{H} frame ({rows * cam.width} px; best run {best[3]} "
+                      f"segments in {best[4]:.2f} s), fp64 oracle restatement (-O3, no FMA), "
+                      f"OpenMP schedule(dynamic,1) over rows on {cores} threads",
+            "runs_mrays_per_s": [round(r[0] / 1e6, 3) for r in runs],
+            "ms_per_frame": round(best[1] / rows * H * 1e3, 2)}
 
 
-def load_traffic(path: str, workload: str, precision: str):
-    """Per-launch HBM bytes measured by rocprofv3 --pmc (profiles/)."""
+def load_profile(path: str, workload: str, precision: str):
+    """Per-launch numbers measured by rocprofv3 --pmc (profiles/)."""
     try:
         with open(path) as fh:
             d = json.load(fh)
-        e = d.get(workload, {}).get(precision)
-        return None if e is None else float(e["hbm_bytes_per_launch"])
-    except (OSError, ValueError, KeyError, TypeError):
+        return d.get(workload, {}).get(precision)
+    except (OSError, ValueError, KeyError, TypeError, AttributeError):
         return None
 
 
@@ -112,18 +132,28 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="c2", choices=sorted(scenes.CONFIGS))
     ap.add_argument("--precision", default="path64", choices=sorted(capi.PRECISIONS))
-    ap.add_argument("--mode", default="frames", choices=["frames", "tiled"])
+    ap.add_argument("--mode", default="tiled", choices=["tiled", "frames"],
+                    help="tiled: one frame per step, row bands across ranks + gather (strong); "
+                         "frames: one frame per rank per step, no collective (weak)")
     ap.add_argument("--out", default="rgb_f32", choices=["rgb_f32", "rgba8"],
                     help="timed output format: linear fp32 RGB (12 B/px, parity buffer) or the "
                          "clamp+truncate RGBA8 epilogue (4 B/px; cuts the tiled gather 3x)")
     ap.add_argument("--frames-in-flight", type=int, default=2,
-                    help="frames mode: consecutive frames go to F output buffers on F streams "
-                         "(a triple-buffered frame loop), so one frame's last waves overlap the "
-                         "next frame's first; 1 = one stream, frames back to back")
+                    help="consecutive frames go to F frame buffers on F streams (double-buffered "
+                         "by default), so one frame's last waves and gather overlap the next "
+                         "frame's render; 1 = one stream, frames back to back")
+    ap.add_argument("--tiler", default="native", choices=["native", "torch"],
+                    help="tiled mode: the C-ABI's rt_multi (RCCL send/recv in C++), or "
+                         "rtamd.tiling over torch.distributed")
+    ap.add_argument("--local-ranks", type=int, default=1,
+                    help="rehearsal only (one process): split the frame over this many ranks "
+                         "on this one GPU with the peer-copy transport; not a measurement")
     ap.add_argument("--sun", action="store_true", help="build-defined sun term (off = parity)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-sweep", action="store_true", help="skip the per-precision kernel sweep")
+    ap.add_argument("--no-sweep", action="store_true",
+                    help="skip the side measurements (precision sweep, sun and moving-camera "
+                         "loops, frame-sharded side run)")
     ap.add_argument("--row-feedback", type=int, default=32,
                     help="RT_OPT_ROW_FEEDBACK: refresh interval (frames) of the measured "
                          "tile-row dispatch order, 0 = off (scheduling only)")
@@ -131,6 +161,7 @@ def main() -> int:
                     help="RT_OPT_BOX_CACHE: reuse the host's per-frame pixel boxes when the "
                          "camera is unchanged (0 = recompute every frame)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--valu-json", default=os.path.join(REPO, "profiles", "pmc_valu.json"))
     args = ap.parse_args()
 
     import torch
@@ -142,8 +173,9 @@ def main() -> int:
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     # RT_BENCH_BACKEND=gloo: rehearsal of the N-rank code path on fewer GPUs than ranks
-    # (ranks share devices round-robin; RCCL refuses two ranks on one GPU).  Not a
-    # measurement: the driver's multi-GPU runs use the default, RCCL ("nccl").
+    # (ranks share devices round-robin; RCCL refuses two ranks on one GPU, so the tiled mode
+    # then uses the torch tiler over gloo).  Not a measurement: the driver's multi-GPU runs
+    # use the default, RCCL ("nccl").
     backend = os.environ.get("RT_BENCH_BACKEND", "nccl")
     if backend == "gloo":
         local %= max(1, torch.cuda.device_count())
@@ -167,99 +199,125 @@ def main() -> int:
     prec = capi.PRECISIONS[args.precision]
     flags = capi.RT_FLAG_SUN if args.sun else 0
     depth = cfg.depth
+    tiled_mode = args.mode == "tiled"
+    tiler = args.tiler if not (tiled_mode and world > 1 and backend == "gloo") else "torch"
 
-    rend = capi.Renderer(local)
+    rend = capi.Renderer(local)   # census, side measurements, frames mode, kernel time
     rend.set_option(capi.RT_OPT_BOX_CACHE, args.box_cache)
     rend.set_option(capi.RT_OPT_ROW_FEEDBACK, args.row_feedback)
     rend.set_scene(prims)
-    cam = capi.camera_init(**scenes.camera_args(cfg.width, cfg.height))
-    W, H = cam.width, cam.height
-    if args.mode == "frames":
-        # frame `rank` of a fly-through: Camera::forward moves position by
-        # forward_vec()*movement_speed = (1,0,0)*0.1 and never re-calls init().
-        cam.position[0] += 0.1 * rank
-        row0, nrows = 0, H
-    else:
-        row0, nrows = capi.band_rows(H, world, rank)
-    band_max = -(-H // world) if args.mode == "tiled" else H
+    cam0 = capi.camera_init(**scenes.camera_args(cfg.width, cfg.height))
+    W, H = cam0.width, cam0.height
+    out_fmt = capi.RT_OUT_RGBA8 if args.out == "rgba8" else capi.RT_OUT_RGB_F32
+    ch, tdt = (4, torch.uint8) if args.out == "rgba8" else (3, torch.float32)
 
-    # dedicated streams: the C-ABI maps a NULL stream to its own, so torch's legacy
-    # default stream (handle 0) would put the launches and the timing events apart
-    fif = max(1, args.frames_in_flight) if args.mode == "frames" else 1
+    # frames mode: frame `rank` of a fly-through (Camera::forward moves position by
+    # forward_vec()*movement_speed = (1,0,0)*0.1 and never re-calls init(), scene.cpp:121)
+    cam_fly = capi.camera_init(**scenes.camera_args(cfg.width, cfg.height))
+    cam_fly.position[0] += 0.1 * rank
+    cam = cam0 if tiled_mode else cam_fly
+    # this rank's rows: its band of the one frame (tiled), or the whole frame (frames)
+    if tiled_mode:
+        row0, nrows = capi.band_rows(H, world, rank)
+    else:
+        row0, nrows = 0, H
+
+    fif = max(1, args.frames_in_flight)
     streams = [torch.cuda.Stream(dev) for _ in range(fif)]
     stream = streams[0]
     torch.cuda.set_stream(stream)
-    # sized for fp32 RGB: the per-precision sweep below always writes 12 B/px into them;
-    # frames in flight: one output buffer per stream (every frame is rendered in full)
-    outs = [torch.empty((band_max, W, 3), dtype=torch.float32, device=dev) for _ in range(fif)]
+    st_ptrs = [s_.cuda_stream for s_ in streams]
+    # frame buffers: the whole frame on rank 0 (tiled: the bands are gathered into it) or on
+    # every rank (frames mode); fp32-RGB sized, which the sweep below also writes
+    full = (not tiled_mode) or rank == 0
+    outs = [torch.empty((H if full else max(1, nrows), W, 3), dtype=torch.float32, device=dev)
+            for _ in range(fif)]
     out = outs[0]
-    out_fmt = capi.RT_OUT_RGBA8 if args.out == "rgba8" else capi.RT_OUT_RGB_F32
+    out_ptrs = [o.data_ptr() for o in outs]
     segs_t = torch.zeros(1, dtype=torch.int64, device=dev)
 
-    def launch(d_segs: int = 0, dst=None, slot: int = 0):
-        rend.render_device(cam, depth, (dst if dst is not None else outs[slot]).data_ptr(), prec,
-                           flags, out_fmt, row0=row0, nrows=nrows, d_segments=d_segs,
-                           stream=streams[slot].cuda_stream)
-
-    tiled = None
-    if args.mode == "tiled" and world > 1:
-        from rtamd import tiling
-        # double-buffered: the gather of frame k (RCCL stream) overlaps the render of k+1
-        tiled = tiling.TiledFrames(lambda r0, n, buf: launch(dst=buf), H, W,
-                                   4 if args.out == "rgba8" else 3,
-                                   torch.uint8 if args.out == "rgba8" else torch.float32,
-                                   dev, depth=2)
-
-    nstep = [0]
-
-    def step():
-        if tiled is not None:
-            tiled.submit()
-        else:
-            launch(slot=nstep[0] % fif)
-            nstep[0] += 1
-
-    out_ptrs = [o.data_ptr() for o in outs]
-    st_ptrs = [s_.cuda_stream for s_ in streams]
-
-    def run_steps(n: int):
-        """n consecutive steps: frames mode enqueues them with ONE C-ABI call
-        (rt_render_device_frames: each frame's own host work and launch, minus the Python
-        per-call overhead, so the host stays ahead of the GPU as a C++ frame loop would)."""
-        if tiled is not None:
-            for _ in range(n):
-                step()
-            return
-        k = nstep[0] % fif
-        rend.render_device_frames([cam], depth, out_ptrs[k:] + out_ptrs[:k], prec, flags,
-                                  out_fmt, row0=row0, nrows=nrows,
-                                  streams=st_ptrs[k:] + st_ptrs[:k], nframes=n)
-        nstep[0] += n
-
-    def join_streams():
-        # stream 0 waits for every other stream's work (the end-of-region event is then
-        # behind every frame of the region)
-        for s_ in streams[1:]:
-            stream.wait_stream(s_)
-
-    # census: exact segment count of this rank's share (untimed)
-    launch(segs_t.data_ptr())
+    # ---- census: exact segment count of this rank's rows (untimed) ----
+    rend.render_device(cam, depth, out.data_ptr(), prec, flags, capi.RT_OUT_RGB_F32, row0=row0,
+                       nrows=nrows, d_segments=segs_t.data_ptr(), stream=stream.cuda_stream)
     torch.cuda.synchronize(dev)
     my_segs = int(segs_t.item())
     tot = torch.tensor([my_segs], dtype=torch.int64, device=dev)
     if world > 1:
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
     total_segs = int(tot.item())
+    frame_segs = total_segs if tiled_mode else my_segs   # one frame
 
-    # Side measurements (per-precision kernel sweep, sun extension, moving camera) run
-    # BEFORE the warmup and the timed region, on every rank (rank 0 reports them).  They
-    # are measurements of their own; running them first also means the timed region
-    # starts on a GPU at its sustained clock, as inside a running frame loop, rather than
-    # on the ramp out of idle (tools/ramp_probe.py: frames 4-255 after idle run ~7%
-    # slower than later ones, so a 20-step region would measure the ramp).
+    # ---- the tiled frame operator ----
+    multi = None
+    torch_tiled = None
+    if tiled_mode and tiler == "native":
+        if world > 1:
+            uid = [capi.multi_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            multi = capi.MultiRenderer([local], nranks=world, first_rank=rank, unique_id=uid[0])
+        elif args.local_ranks > 1:
+            multi = capi.MultiRenderer([local] * args.local_ranks,
+                                       transport=capi.RT_TRANSPORT_COPY)
+        else:
+            multi = capi.MultiRenderer([local])
+        multi.set_option(capi.RT_OPT_BOX_CACHE, args.box_cache)
+        multi.set_option(capi.RT_OPT_ROW_FEEDBACK, args.row_feedback)
+        multi.set_scene(prims)
+    elif tiled_mode:
+        from rtamd import tiling
+        # double-buffered: the gather of frame k (collective stream) overlaps the render of k+1
+        band_max = -(-H // world)
+        band_bufs = [torch.empty((band_max, W, ch), dtype=tdt, device=dev)]
+        torch_tiled = tiling.TiledFrames(
+            lambda r0, n, buf: rend.render_device(cam, depth, buf.data_ptr(), prec, flags, out_fmt,
+                                                  row0=r0, nrows=n, stream=stream.cuda_stream),
+            H, W, ch, tdt, dev, depth=2)
+        del band_bufs
+
+    def run_steps(n: int):
+        """n consecutive frames, enqueued by ONE C-ABI call (or the torch tiler's loop)."""
+        if multi is not None:
+            if multi.has_root:
+                multi.render_device_frames([cam], depth, out_ptrs, prec, flags, out_fmt,
+                                           streams=st_ptrs, nframes=n)
+            else:   # non-root ranks: the band renders and sends; stream 0 waits for the sends
+                multi.render_device_frames([cam], depth, [], prec, flags, out_fmt,
+                                           streams=st_ptrs[:1], nframes=n)
+        elif torch_tiled is not None:
+            for _ in range(n):
+                torch_tiled.submit()
+            torch_tiled.drain()
+        else:
+            rend.render_device_frames([cam], depth, out_ptrs, prec, flags, out_fmt, row0=row0,
+                                      nrows=nrows, streams=st_ptrs, nframes=n)
+
+    def join_streams():
+        for s_ in streams[1:]:
+            stream.wait_stream(s_)
+
+    def timed_frames(cams, nframes, fl, nrep=2):
+        """Best ms/frame of nframes frames of `cams` (cycled) through the frames-in-flight
+        loop on this rank's rows (HIP events on stream 0, every stream joined)."""
+        best = None
+        for _ in range(nrep):
+            torch.cuda.synchronize(dev)
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for s_ in streams[1:]:
+                s_.wait_stream(stream)
+            rend.render_device_frames(cams, depth, out_ptrs, prec, fl, capi.RT_OUT_RGB_F32,
+                                      row0=row0, nrows=nrows, streams=st_ptrs, nframes=nframes)
+            join_streams()
+            e1.record(stream)
+            torch.cuda.synchronize(dev)
+            ms = e0.elapsed_time(e1) / nframes
+            best = ms if best is None else min(best, ms)
+        return best
+
+    # ---- side measurements (before the timed region; rank 0 reports) ----
     nsw = 200
-    sweep = {}
-    sun_ext = None
+    sweep, sun_ext, moving = {}, None, None
     if not args.no_sweep:
         for pname, pc in capi.PRECISIONS.items():
             e0 = torch.cuda.Event(enable_timing=True)
@@ -276,84 +334,70 @@ def main() -> int:
             sweep[pname] = {"kernel_ms": round(kms, 4),
                             "mrays_per_s": round(my_segs / (kms * 1e-3) / 1e6, 1),
                             "dtype": DTYPE[pname], "parity": PARITY[pname]}
-        if not args.sun:
-            # config 2's "sun" is reported as a separate extension run (same ray
-            # paths and segment count; the sun only adds shading terms)
-            e0 = torch.cuda.Event(enable_timing=True)
-            e1 = torch.cuda.Event(enable_timing=True)
-            rend.render_device(cam, depth, out.data_ptr(), prec, capi.RT_FLAG_SUN,
-                               capi.RT_OUT_RGB_F32, row0=row0, nrows=nrows, stream=stream.cuda_stream)
-            e0.record(stream)
-            for _ in range(nsw):
-                rend.render_device(cam, depth, out.data_ptr(), prec, capi.RT_FLAG_SUN,
-                                   capi.RT_OUT_RGB_F32, row0=row0, nrows=nrows,
-                                   stream=stream.cuda_stream)
-            e1.record(stream)
-            torch.cuda.synchronize(dev)
-            kms = e0.elapsed_time(e1) / nsw
-            sun_ext = {"precision": args.precision, "kernel_ms": round(kms, 4),
-                       "mrays_per_s": round(my_segs / (kms * 1e-3) / 1e6, 1),
+        if not args.sun and rank == 0 and world == 1:
+            # config 2's literal "+ sun": the same frame loop as the headline (frames in
+            # flight, fp32 RGB) with the build-defined sun term on — same ray paths and
+            # segment count (the sun only adds shading terms)
+            ms = timed_frames([cam], nsw, capi.RT_FLAG_SUN)
+            sun_ext = {"precision": args.precision, "ms_per_frame": round(ms, 4),
+                       "mrays_per_s": round(my_segs / (ms * 1e-3) / 1e6, 1),
+                       "frames_in_flight": fif, "frames": nsw,
                        "parity": "sun term is build-defined (constants main.cpp:18-19, unused "
                                  "by the reference): pinned to the oracle, not the reference"}
+        if rank == 0 and world == 1:
+            # a camera moving every frame (a fly-through of 200 frames, 0.01 scene units per
+            # frame along +x: rays travel toward +x, main.cpp:133) through the same
+            # frames-in-flight loop, with the measured row order refreshed every
+            # RT_OPT_ROW_FEEDBACK frames (so it lags the view) and off
+            ca = scenes.camera_args(W, H)
+            cams = []
+            for f in range(200):
+                a = dict(ca)
+                a["position"] = (ca["position"][0] + 0.01 * f, ca["position"][1], ca["position"][2])
+                a["lookat"] = (ca["lookat"][0] + 0.01 * f, ca["lookat"][1], ca["lookat"][2])
+                cams.append(capi.camera_init(**a))
+            segs_t.zero_()
+            for c in cams:   # census of the 200 frames (untimed)
+                rend.render_device(c, depth, out.data_ptr(), prec, flags, capi.RT_OUT_RGB_F32,
+                                   row0=row0, nrows=nrows, d_segments=segs_t.data_ptr(),
+                                   stream=stream.cuda_stream)
+            torch.cuda.synchronize(dev)
+            mv_segs = int(segs_t.item())
+            moving = {"frames": len(cams), "step": "0.01 units/frame along +x",
+                      "frames_in_flight": fif, "segments": mv_segs}
+            for fb in (0, args.row_feedback):
+                rend.set_option(capi.RT_OPT_ROW_FEEDBACK, fb)
+                ms = timed_frames(cams, len(cams), flags)
+                moving[f"ms_per_frame_row_feedback_{fb}"] = round(ms, 4)
+                moving[f"mrays_per_s_row_feedback_{fb}"] = round(
+                    mv_segs / len(cams) / (ms * 1e-3) / 1e6, 1)
+            rend.set_option(capi.RT_OPT_ROW_FEEDBACK, args.row_feedback)
 
-    moving = None
-    if not args.no_sweep and args.mode == "frames":
-        # the measured tile-row order on a camera that moves every frame (a fly-through of
-        # 200 frames, 0.01 scene units per frame toward the scene — rays travel toward +x,
-        # main.cpp:133): the order is refreshed every RT_OPT_ROW_FEEDBACK frames, so it
-        # lags the view; per-frame ms with the feedback on and off (kernel stream time)
-        ca = scenes.camera_args(W, H)
-        cams = []
-        for f in range(200):
-            dx = 0.01 * f
-            a = dict(ca)
-            a["position"] = (ca["position"][0] + dx, ca["position"][1], ca["position"][2])
-            a["lookat"] = (ca["lookat"][0] + dx, ca["lookat"][1], ca["lookat"][2])
-            cams.append(capi.camera_init(**a))
-        moving = {"frames": len(cams), "step": "0.01 units/frame along +x"}
-        for fb in (0, args.row_feedback):
-            rend.set_option(capi.RT_OPT_ROW_FEEDBACK, fb)
-            best = None
-            for _ in range(2):
-                e0 = torch.cuda.Event(enable_timing=True)
-                e1 = torch.cuda.Event(enable_timing=True)
-                e0.record(stream)
-                for c in cams:
-                    rend.render_device(c, depth, out.data_ptr(), prec, flags, capi.RT_OUT_RGB_F32,
-                                       row0=row0, nrows=nrows, stream=stream.cuda_stream)
-                e1.record(stream)
-                torch.cuda.synchronize(dev)
-                ms = e0.elapsed_time(e1) / len(cams)
-                best = ms if best is None else min(best, ms)
-            moving[f"ms_per_frame_row_feedback_{fb}"] = round(best, 4)
-        rend.set_option(capi.RT_OPT_ROW_FEEDBACK, args.row_feedback)
-
-    # the moving camera left the row feedback holding another view's order: drop it (with
-    # any snapshot still in flight), so the first warmup frame samples this camera afresh,
-    # with frames in flight as the timed steps run them.  (Measured with 20-step regions,
-    # interleaved on one box: an order sampled from isolated launches — synchronous census
-    # frames, or the sweep's back-to-back frames — runs the frames-in-flight loop 4-8%
-    # slower on average and erratically (78-120 Grays/s); one sampled among frames in
-    # flight gives 116-121; more back-to-back samples inside a 20-step region cost more than
-    # they gain.)
+    # the side loops left the row feedback holding another view's order: drop it (with any
+    # snapshot still in flight), so the first warmup frame samples this camera afresh, with
+    # frames in flight as the timed steps run them
     rend.set_option(capi.RT_OPT_ROW_FEEDBACK, 0)
     rend.set_option(capi.RT_OPT_ROW_FEEDBACK, args.row_feedback)
 
+    # ---- warmup + timed region ----
     run_steps(args.warmup)
-    if tiled is not None:
-        tiled.drain()
+    torch.cuda.synchronize(dev)
+    if multi is not None:
+        multi.sync()
     barrier()
     torch.cuda.synchronize(dev)
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(stream)
+    for s_ in streams[1:]:
+        s_.wait_stream(stream)
     run_steps(args.steps)
-    if tiled is not None:
-        tiled.drain()
     join_streams()
     ev1.record(stream)
     torch.cuda.synchronize(dev)
+    if multi is not None:
+        multi.sync()
     barrier()
     t1 = time.perf_counter()
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
@@ -362,7 +406,7 @@ def main() -> int:
     elapsed_s = float(elapsed.item())
     stream_ms = ev0.elapsed_time(ev1) / args.steps
 
-    # per-launch kernel time: one stream, launches back to back (HIP events on that stream)
+    # ---- per-launch kernel time: this rank's rows, one stream, launches back to back ----
     ek0 = torch.cuda.Event(enable_timing=True)
     ek1 = torch.cuda.Event(enable_timing=True)
     nk = max(10, args.steps)
@@ -373,21 +417,65 @@ def main() -> int:
     torch.cuda.synchronize(dev)
     kernel_ms = ek0.elapsed_time(ek1) / nk
 
+    # ---- N > 1 side run: the weak (frame-sharded) layout, same frame loop, no collective --
+    sharded = None
+    if tiled_mode and world > 1 and not args.no_sweep:
+        segs_t.zero_()
+        rend.render_device(cam_fly, depth, out.data_ptr(), prec, flags, capi.RT_OUT_RGB_F32,
+                           d_segments=segs_t.data_ptr(), stream=stream.cuda_stream)
+        torch.cuda.synchronize(dev)
+        t_segs = segs_t.clone()
+        dist.all_reduce(t_segs, op=dist.ReduceOp.SUM)
+        if full:
+            fl_outs = out_ptrs
+        else:
+            fl_bufs = [torch.empty((H, W, 3), dtype=torch.float32, device=dev) for _ in range(fif)]
+            fl_outs = [b.data_ptr() for b in fl_bufs]
+        nfs = max(20, args.steps // 2)
+        rend.render_device_frames([cam_fly], depth, fl_outs, prec, flags, out_fmt,
+                                  streams=st_ptrs, nframes=args.warmup)
+        torch.cuda.synchronize(dev)
+        barrier()
+        ts0 = time.perf_counter()
+        rend.render_device_frames([cam_fly], depth, fl_outs, prec, flags, out_fmt,
+                                  streams=st_ptrs, nframes=nfs)
+        torch.cuda.synchronize(dev)
+        barrier()
+        ts = torch.tensor([time.perf_counter() - ts0], dtype=torch.float64, device=dev)
+        dist.all_reduce(ts, op=dist.ReduceOp.MAX)
+        sharded = {"value": round(int(t_segs.item()) * nfs / float(ts.item()) / 1e6, 2),
+                   "unit": "Mrays/s", "scaling": "weak", "frames_per_step": world,
+                   "ms_per_step": round(float(ts.item()) / nfs * 1e3, 4),
+                   "parallelism": f"frame-sharded x{world} (fly-through, no collective)"}
+
     result = None
     if rank == 0:
         ms_step = elapsed_s / args.steps * 1e3
         value = total_segs * args.steps / elapsed_s / 1e6
-        frames_per_step = world if args.mode == "frames" else 1
+        frames_per_step = 1 if tiled_mode else world
         px_step = W * H * frames_per_step
         kernel_s = kernel_ms * 1e-3
         out_bytes = nrows * W * (4 if args.out == "rgba8" else 12)
         alg_bytes = out_bytes + scene_bytes(n_sph, n_wall, len(sc))
-        workload = f"{cfg.name}:{W}x{H}:d{depth}:s{n_sph}w{n_wall}"
-        # PMC traffic was collected on the fp32 RGB output only
-        traffic = (load_traffic(args.traffic_json, workload, args.precision)
-                   if args.out == "rgb_f32" else None)
+        tag = cfg.name if not (tiled_mode and world > 1) else "c4"
+        workload = f"{tag}:{W}x{H}:d{depth}:s{n_sph}w{n_wall}"
+        kern_workload = f"{cfg.name}:{W}x{H}:d{depth}:s{n_sph}w{n_wall}"
+        # PMC was collected on the one-GPU kernel (the whole frame, fp32 RGB output); a
+        # 1/N band's kernel is not the profiled one
+        traffic = None
+        if args.out == "rgb_f32" and nrows == H:
+            e = load_profile(args.traffic_json, kern_workload, args.precision)
+            traffic = None if e is None else float(e["hbm_bytes_per_launch"])
+        valu_hw = load_profile(args.valu_json, kern_workload, args.precision) if nrows == H else None
         flops = my_segs * flop_per_segment(n_sph, n_wall)
         valu_peak = VALU_PEAK_TFLOPS[args.precision]
+        if tiled_mode:
+            par = (f"row-tiled x{world} + gather ({'RCCL send/recv, rt_multi' if multi is not None else 'torch.distributed ' + backend})"
+                   if world > 1 else "one GPU (the one band is the whole frame)")
+            if args.local_ranks > 1:
+                par = f"REHEARSAL: {args.local_ranks} ranks on one GPU, peer copies"
+        else:
+            par = f"frame-sharded x{world}"
         result = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -397,7 +485,7 @@ def main() -> int:
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 4),
             "higher_is_better": True,
-            "scaling": "weak" if args.mode == "frames" else "strong",
+            "scaling": "strong" if tiled_mode else "weak",
             "vs_baseline": None,
             "dtype": DTYPE[args.precision],
             "data": "synthetic",
@@ -412,17 +500,17 @@ def main() -> int:
                 "frames_per_step": frames_per_step,
                 "segments_per_step": total_segs,
                 "segments_per_pixel": round(total_segs / px_step, 4),
-                "parallelism": (f"frame-sharded x{world}" if args.mode == "frames"
-                                else f"row-tiled x{world} + gather"),
+                "parallelism": par,
+                "band_rows_rank0": nrows,
                 "host_box_cache": bool(args.box_cache),
                 "row_feedback": args.row_feedback,
                 "frames_in_flight": fif,
                 "backend": backend if world > 1 else None,
             },
-            "ms_per_frame": round(ms_step / frames_per_step if args.mode == "frames" else ms_step, 4),
+            "ms_per_frame": round(ms_step / frames_per_step, 4),
             "mpx_per_s": round(px_step * args.steps / elapsed_s / 1e6, 2),
-            # one frame at a time on one stream (HIP events around back-to-back launches):
-            # the per-frame latency, and the kernel duration the rooflines are priced on
+            # one frame (this rank's rows) at a time on one stream (HIP events around
+            # back-to-back launches): the per-frame latency the rooflines are priced on
             "kernel_ms": round(kernel_ms, 4),
             "stream_ms_per_step": round(stream_ms, 4),
             "roofline": {
@@ -442,16 +530,23 @@ def main() -> int:
                 "unit": "TFLOP/s",
                 "frac": round(flops / kernel_s / 1e12 / valu_peak, 4),
                 "flop_per_launch": flops,
-                "convention": "SURVEY 8d: F_seg = 30*N_sphere + 38*N_wall + 60, FMA = 2",
+                "convention": "SURVEY 8d: F_seg = 30*N_sphere + 38*N_wall + 60, FMA = 2 — "
+                              "algorithmic-equivalent: it prices a full linear scan, while "
+                              "the kernels cull (tile bins, cone, clusters), so it credits "
+                              "work never executed (c5 gives 1.26x peak); `hw` is measured",
+                "hw": valu_hw,
             },
             "cpu_baseline": None,
             "precision_sweep": sweep or None,
             "sun_extension": sun_ext,
             "moving_camera": moving,
+            "frame_sharded": sharded,
         }
         if world == 1 and not args.no_cpu_baseline and args.cpu_seconds > 0:
-            result["cpu_baseline"] = cpu_baseline(cfg, prims, cam, depth, flags, args.cpu_seconds)
+            result["cpu_baseline"] = cpu_baseline(cfg, prims, cam0, depth, flags, args.cpu_seconds)
         print(json.dumps(result), flush=True)
+    if multi is not None:
+        multi.close()
     rend.close()
     if world > 1:
         dist.destroy_process_group()

@@ -60,7 +60,10 @@ struct Material {
 };
 
 /* The primitive plugin interface (scene.h:51-60).  pack() is the hook the GPU path
- * needs: it writes the object's state into a flat rt_prim record. */
+ * needs: it writes the object's state into a flat rt_prim record.  It is not pure, so a
+ * subclass written against the reference's interface (intersect only) still compiles; the
+ * default throws std::invalid_argument ("unsupported primitive"), which rt_scene lets
+ * through before any device work — the kernels know spheres and walls only. */
 class SceneGeometry {
     Material mat;
 
@@ -68,7 +71,7 @@ public:
     explicit SceneGeometry(Material mat) : mat(mat) {}
     virtual ~SceneGeometry() {}
     virtual Collision intersect(ray r) const = 0;
-    virtual void pack(rt_prim* out) const = 0;
+    virtual void pack(rt_prim* out) const;
     Material get_material() const { return mat; }
 
 protected:
@@ -134,12 +137,17 @@ void rt_scene(std::vector<vec3> u, const std::vector<std::unique_ptr<SceneGeomet
 
 /* Options of the GPU frame operator (not in the reference): device, precision
  * (RT_PREC_*; default RT_PREC_MIXED whose output equals the fp64 path), recursion
- * depth (default 10) and flags (RT_FLAG_SUN). */
+ * depth (default 10) and flags (RT_FLAG_SUN).  `devices` with more than one entry renders
+ * every frame row-tiled across those GPUs and gathers it into devices[0] (rt_multi_*,
+ * BASELINE config 4; `transport` RT_TRANSPORT_RCCL, or RT_TRANSPORT_COPY, which also takes
+ * one GPU listed several times); the frame is bitwise the one-GPU frame. */
 struct RtSceneOptions {
     int device = 0;
     int precision = RT_PREC_MIXED;
     int depth = 10;
     unsigned flags = 0;
+    std::vector<int> devices;
+    int transport = RT_TRANSPORT_RCCL;
 };
 void rt_scene_set_options(const RtSceneOptions& opts);
 RtSceneOptions rt_scene_get_options();

@@ -30,7 +30,9 @@
 extern "C" {
 #endif
 
-#define RT_CAPI_VERSION 1
+/* Version 2 adds the multi-GPU frame operator (rt_multi_*) and RT_ERR_COMM; every version-1
+ * entry point keeps its signature and meaning (the ABI grows additively). */
+#define RT_CAPI_VERSION 2
 
 /* ---- status codes ------------------------------------------------------- */
 enum rt_status {
@@ -41,7 +43,8 @@ enum rt_status {
     RT_ERR_OUT_OF_MEMORY = 4,
     RT_ERR_NO_SCENE = 5,      /* rt_render* before rt_set_scene */
     RT_ERR_UNSUPPORTED = 6,   /* depth / flag combination this build does not ship */
-    RT_ERR_OUT_OF_RANGE = 7   /* row band outside the image (reference: std::out_of_range) */
+    RT_ERR_OUT_OF_RANGE = 7,  /* row band outside the image (reference: std::out_of_range) */
+    RT_ERR_COMM = 8           /* an RCCL call failed (rt_multi_last_error names it) */
 };
 
 /* ---- scene records (reference scene.h:35-84) ---------------------------- */
@@ -194,7 +197,8 @@ enum rt_option {
                                          order (measured: c2 +1% with the order).  Output is
                                          identical (wall ties compare scene indices). */
     RT_OPT_CLUSTER_COS = 12           /* C in [-2000, 2000] (default 400): in scenes that use
-                                         the wave cull, a RT_PREC_PATH64 wave whose live
+                                         the wave cull, a RT_PREC_PATH64 or RT_PREC_F32
+                                         wave (their cull kernels) whose live
                                          rays' cone has cos(half-angle) < C/1000 tests each
                                          lane's own ray against sphere clusters (boxes of
                                          <= 8 spheres) and runs the exact test on its own
@@ -239,6 +243,80 @@ int rt_render_device_frames(rt_ctx* ctx, const rt_camera* cams, int32_t ncams, i
                             int32_t nrows, int32_t depth, int32_t precision, uint32_t flags,
                             int32_t out_format, void* const* d_outs, int32_t nouts,
                             void* const* streams, int32_t nstreams, int32_t nframes);
+
+/* ---- multi-GPU frame operator (BASELINE config 4) ----------------------- */
+/* ONE frame split into contiguous row bands (rt_band_rows) over nranks ranks, one GPU each,
+ * every band rendered by that rank's own rt_ctx, then gathered into the frame buffer of
+ * rank 0 (the root) — the reference renders the frame on one CPU thread (main.cpp:124-139,
+ * called at main.cpp:329); pixels are independent, so the gathered frame is bitwise the
+ * one-GPU frame.  Two process models, one object:
+ *   - one process drives every GPU: nlocal == nranks, first_rank 0, unique_id NULL
+ *     (the communicator is made as ncclCommInitAll would; one host worker thread per extra
+ *     device does that rank's per-frame host work and launches in parallel);
+ *   - one process per GPU (torchrun-style): nlocal == 1, first_rank = this process's rank,
+ *     unique_id = the RT_MULTI_ID_BYTES bytes rt_multi_unique_id returned on ONE process
+ *     and shared with the others (ncclCommInitRank; blocks until every rank has joined).
+ * Transports: RT_TRANSPORT_RCCL gathers with ncclSend/ncclRecv (rccl.h) over xGMI —
+ * bands may differ in height by one row, so no padding; RT_TRANSPORT_COPY (one process
+ * only) copies each band into the root's frame with hipMemcpyPeerAsync and also accepts
+ * the same device more than once (several ranks on one GPU: the orchestration without
+ * RCCL, e.g. on a one-GPU machine).
+ * Frames in flight: each non-root rank renders into one of RT_MULTI_SLOTS band buffers on
+ * its render stream while the previous frame's band is still being sent on its comm stream;
+ * a band buffer is reused only after its send has completed (device-side event waits; the
+ * host never blocks in rt_multi_render_device*). */
+#define RT_MULTI_ID_BYTES 128
+#define RT_MULTI_SLOTS 2
+enum rt_transport {
+    RT_TRANSPORT_RCCL = 0,
+    RT_TRANSPORT_COPY = 1
+};
+typedef struct rt_multi rt_multi;
+
+/* A fresh communicator id (ncclGetUniqueId) for the one-process-per-GPU model. */
+int rt_multi_unique_id(uint8_t id[RT_MULTI_ID_BYTES]);
+
+/* devices[nlocal]: the HIP device of each local rank (global ranks first_rank ..
+ * first_rank + nlocal - 1 of nranks).  RT_ERR_NO_DEVICE for a device index out of range,
+ * RT_ERR_UNSUPPORTED for RT_TRANSPORT_RCCL with a device listed twice or
+ * RT_TRANSPORT_COPY across processes, RT_ERR_COMM if RCCL fails. */
+int rt_multi_create(const int32_t* devices, int32_t nlocal, int32_t nranks, int32_t first_rank,
+                    const uint8_t* unique_id, int32_t transport, rt_multi** out);
+int rt_multi_destroy(rt_multi* m);
+const char* rt_multi_last_error(const rt_multi* m);
+
+/* rt_set_scene / rt_set_option on every local rank's ctx (each rank keeps its own per-band
+ * state: tile boxes, measured row order). */
+int rt_multi_set_scene(rt_multi* m, const rt_prim* prims, int32_t n);
+int rt_multi_set_option(rt_multi* m, int32_t option, int64_t value);
+
+/* Enqueue one frame.  d_frame: on the process holding the root, DEVICE memory on the root's
+ * device of height x width pixels of out_format (the root's band is rendered into it in
+ * place, the other bands are received into their rows); NULL on other processes.  stream
+ * (a hipStream_t on the root's device; NULL = the root ctx's stream): the frame's work
+ * starts after the work already on it, and work enqueued on it later sees the complete
+ * frame.  On a process without the root, a non-NULL stream (on that rank's device) waits for
+ * the rank's band to have been sent.  No host synchronisation. */
+int rt_multi_render_device(rt_multi* m, const rt_camera* cam, int32_t depth, int32_t precision,
+                           uint32_t flags, int32_t out_format, void* d_frame, void* stream);
+
+/* nframes frames as rt_multi_render_device calls in order would enqueue them: frame f
+ * renders cams[f % ncams] into d_frames[f % nbufs] on streams[f % nstreams]. */
+int rt_multi_render_device_frames(rt_multi* m, const rt_camera* cams, int32_t ncams,
+                                  int32_t depth, int32_t precision, uint32_t flags,
+                                  int32_t out_format, void* const* d_frames, int32_t nbufs,
+                                  void* const* streams, int32_t nstreams, int32_t nframes);
+
+/* Synchronous: the gathered frame in caller-owned HOST memory `out` (height x width pixels
+ * of out_format) on the process holding the root (out may be NULL elsewhere).
+ * stats->ms = device time from the start of the frame's work to the complete frame on the
+ * root (render + gather); stats->segments is not counted (0). */
+int rt_multi_render(rt_multi* m, const rt_camera* cam, int32_t depth, int32_t precision,
+                    uint32_t flags, int32_t out_format, void* out, rt_stats* stats);
+
+/* Waits for every frame this process enqueued; RT_ERR_COMM if RCCL reported an
+ * asynchronous error. */
+int rt_multi_sync(rt_multi* m);
 
 /* ---- host helpers (restatements the host side of rt_scene needs) -------- */
 /* Camera::init (scene.cpp:80-106) in fp64: fills cam from the Camera fields.

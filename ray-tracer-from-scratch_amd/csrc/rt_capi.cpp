@@ -930,6 +930,7 @@ const char* rt_strerror(int status) {
         case RT_ERR_NO_SCENE: return "no scene uploaded";
         case RT_ERR_UNSUPPORTED: return "unsupported depth/flags";
         case RT_ERR_OUT_OF_RANGE: return "row band out of range";
+        case RT_ERR_COMM: return "RCCL communication error";
         default: return "unknown status";
     }
 }

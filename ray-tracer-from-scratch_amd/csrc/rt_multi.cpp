@@ -1,0 +1,582 @@
+/*
+ * rt_multi.cpp — the multi-GPU frame operator of include/rt_capi.h (rt_multi_*):
+ * BASELINE config 4, one frame split into contiguous row bands across GPUs and gathered
+ * into rank 0's frame buffer.
+ *
+ * The reference renders every frame on one CPU thread (rt_scene, main.cpp:124-139, called
+ * from the event loop at main.cpp:329) and has no multi-device path; this file
+ * is the build's one exchange step.  It sits ABOVE the single-GPU C-ABI: every rank is a
+ * plain rt_ctx driven through rt_set_scene / rt_set_option / rt_render_device, so a band
+ * is rendered by exactly the kernels and host work of a one-GPU render of those rows, and
+ * the gathered frame is bitwise the one-GPU frame (pixels are independent).
+ *
+ * Per frame and rank (stream order does the synchronisation; the host never waits):
+ *   root (global rank 0): its band is rendered in place into the caller's frame buffer on
+ *     the caller's stream; RCCL: the comm stream waits for the caller's earlier work (the
+ *     buffer may still be read), receives every other band into its rows (one
+ *     ncclGroupStart/End), and the caller's stream waits for it.
+ *   other ranks: the render stream waits until band buffer `slot` has been sent (frame
+ *     k - RT_MULTI_SLOTS), renders the band into it, and the comm stream sends it once the
+ *     render is done (RCCL ncclSend, or a peer copy into the root's rows for
+ *     RT_TRANSPORT_COPY) — so the render of frame k+1 overlaps the send of frame k.
+ * One process driving several GPUs runs the extra ranks' host work (pixel boxes, row order,
+ * launch: rt_render_device) on one worker thread per rank, in parallel with the caller's
+ * thread, which does the root's.
+ */
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <thread>
+#include <vector>
+
+#include "../../include/rt_capi.h"
+
+namespace {
+
+struct Rank;
+
+struct Job {
+    const rt_camera* cam = nullptr;
+    int32_t depth = 0, precision = 0, out_format = 0;
+    uint32_t flags = 0;
+    char* d_frame = nullptr;        // root's frame buffer (root rank's job, COPY targets)
+    hipStream_t stream = nullptr;   // caller stream (root's device, or this rank's device)
+    hipEvent_t ev_in = nullptr;     // recorded on the caller's stream before the frame
+    int slot = 0;
+};
+
+struct Rank {
+    int rank = 0;                   // global rank
+    int device = 0;
+    rt_ctx* ctx = nullptr;
+    ncclComm_t comm = nullptr;
+    hipStream_t render_stream = nullptr, comm_stream = nullptr;
+    void* band[RT_MULTI_SLOTS] = {nullptr, nullptr};
+    size_t band_cap = 0;
+    hipEvent_t ev_rendered[RT_MULTI_SLOTS] = {nullptr, nullptr};
+    hipEvent_t ev_sent[RT_MULTI_SLOTS] = {nullptr, nullptr};
+    hipEvent_t ev_done = nullptr;   // root, RCCL: every band received
+    // worker thread (local ranks other than the first, one process driving several GPUs)
+    std::thread th;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::atomic<uint64_t> posted{0}, finished{0};
+    bool quit = false;
+    Job job;
+    int status = RT_OK;
+};
+
+}  // namespace
+
+struct rt_multi {
+    int nranks = 1, nlocal = 1, first_rank = 0, transport = RT_TRANSPORT_RCCL;
+    std::vector<Rank*> r;           // local ranks, r[0] = first_rank
+    uint64_t frame = 0;
+    hipEvent_t ev_in[RT_MULTI_SLOTS] = {nullptr, nullptr};  // root's device (process with root)
+    hipStream_t host_stream = nullptr;                       // rt_multi_render (root's device)
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    void* d_frame = nullptr;
+    size_t d_frame_cap = 0;
+    char last_err[320] = {0};
+    bool has_root() const { return first_rank == 0; }
+};
+
+namespace {
+
+struct DevGuard {  // the caller's current device is restored on every return path
+    int prev = -1;
+    hipError_t err = hipSuccess;
+    explicit DevGuard(int d) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != d) err = hipSetDevice(d);
+    }
+    ~DevGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+int hip_err(rt_multi* m, hipError_t e, const char* what) {
+    if (m) std::snprintf(m->last_err, sizeof m->last_err, "%s: %s", what, hipGetErrorString(e));
+    return e == hipErrorOutOfMemory ? RT_ERR_OUT_OF_MEMORY : RT_ERR_HIP;
+}
+int nccl_err(rt_multi* m, ncclResult_t e, const char* what) {
+    if (m) std::snprintf(m->last_err, sizeof m->last_err, "%s: %s", what, ncclGetErrorString(e));
+    return RT_ERR_COMM;
+}
+int ctx_err(rt_multi* m, const Rank* k, int st, const char* what) {
+    if (m && st != RT_OK)
+        std::snprintf(m->last_err, sizeof m->last_err, "%s (rank %d): %s %s", what, k->rank,
+                      rt_strerror(st), k->ctx ? rt_last_hip_error(k->ctx) : "");
+    return st;
+}
+
+#define MHIP(m, call)                                          \
+    do {                                                       \
+        hipError_t e_ = (call);                                \
+        if (e_ != hipSuccess) return hip_err((m), e_, #call);  \
+    } while (0)
+#define MNCCL(m, call)                                           \
+    do {                                                         \
+        ncclResult_t e_ = (call);                                \
+        if (e_ != ncclSuccess) return nccl_err((m), e_, #call);  \
+    } while (0)
+
+int bpp(int32_t f) { return rt_out_bytes_per_pixel(f); }
+
+/* Band buffers of a non-root rank, grown (rarely) to `bytes` each. */
+int ensure_bands(rt_multi* m, Rank* k, size_t bytes) {
+    if (bytes <= k->band_cap) return RT_OK;
+    // nothing in flight may still read or write the old buffers
+    MHIP(m, hipStreamSynchronize(k->render_stream));
+    MHIP(m, hipStreamSynchronize(k->comm_stream));
+    for (auto& b : k->band) {
+        if (b) MHIP(m, hipFree(b));
+        b = nullptr;
+    }
+    k->band_cap = 0;
+    for (auto& b : k->band) MHIP(m, hipMalloc(&b, bytes));
+    k->band_cap = bytes;
+    return RT_OK;
+}
+
+/* One rank's share of one frame (see the file comment).  Runs on the caller's thread for
+ * the first local rank and on the rank's worker thread for the others. */
+int enqueue_rank(rt_multi* m, Rank* k, const Job& j) {
+    DevGuard dg(k->device);
+    MHIP(m, dg.err);
+    const rt_camera& cam = *j.cam;
+    const size_t row_bytes = (size_t)cam.width * bpp(j.out_format);
+    int32_t row0 = 0, nrows = 0;
+    int st = rt_band_rows(cam.height, m->nranks, k->rank, &row0, &nrows);
+    if (st != RT_OK) return st;
+    const int s = j.slot;
+    if (k->rank == 0) {
+        // the root's band, in place, on the caller's stream
+        if (nrows > 0) {
+            st = rt_render_device(k->ctx, &cam, row0, nrows, j.depth, j.precision, j.flags,
+                                  j.out_format, j.d_frame + (size_t)row0 * row_bytes, nullptr,
+                                  j.stream);
+            if (st != RT_OK) return ctx_err(m, k, st, "rt_render_device");
+        }
+        if (m->transport == RT_TRANSPORT_RCCL && m->nranks > 1) {
+            MHIP(m, hipStreamWaitEvent(k->comm_stream, j.ev_in, 0));
+            MNCCL(m, ncclGroupStart());
+            for (int g = 1; g < m->nranks; g++) {
+                int32_t r0 = 0, nr = 0;
+                (void)rt_band_rows(cam.height, m->nranks, g, &r0, &nr);
+                if (nr <= 0 || row_bytes == 0) continue;
+                const ncclResult_t e = ncclRecv(j.d_frame + (size_t)r0 * row_bytes, (size_t)nr * row_bytes,
+                                                ncclUint8, g, k->comm, k->comm_stream);
+                if (e != ncclSuccess) {
+                    (void)ncclGroupEnd();
+                    return nccl_err(m, e, "ncclRecv");
+                }
+            }
+            MNCCL(m, ncclGroupEnd());
+            MHIP(m, hipEventRecord(k->ev_done, k->comm_stream));
+        }
+        return RT_OK;
+    }
+    const size_t bytes = (size_t)nrows * row_bytes;
+    if (bytes == 0) return RT_OK;  // an empty band (height < nranks): nothing to render or send
+    st = ensure_bands(m, k, (size_t)((cam.height + m->nranks - 1) / m->nranks) * row_bytes);
+    if (st != RT_OK) return st;
+    // band buffer `s` is free once the send of frame k - RT_MULTI_SLOTS has completed
+    MHIP(m, hipStreamWaitEvent(k->render_stream, k->ev_sent[s], 0));
+    st = rt_render_device(k->ctx, &cam, row0, nrows, j.depth, j.precision, j.flags, j.out_format,
+                          k->band[s], nullptr, k->render_stream);
+    if (st != RT_OK) return ctx_err(m, k, st, "rt_render_device");
+    MHIP(m, hipEventRecord(k->ev_rendered[s], k->render_stream));
+    MHIP(m, hipStreamWaitEvent(k->comm_stream, k->ev_rendered[s], 0));
+    if (m->transport == RT_TRANSPORT_RCCL) {
+        MNCCL(m, ncclSend(k->band[s], bytes, ncclUint8, 0, k->comm, k->comm_stream));
+    } else {
+        // the root's rows may still be read by the caller's earlier work on the frame buffer
+        MHIP(m, hipStreamWaitEvent(k->comm_stream, j.ev_in, 0));
+        MHIP(m, hipMemcpyPeerAsync(j.d_frame + (size_t)row0 * row_bytes, m->r[0]->device, k->band[s],
+                                   k->device, bytes, k->comm_stream));
+    }
+    MHIP(m, hipEventRecord(k->ev_sent[s], k->comm_stream));
+    if (j.stream && m->transport == RT_TRANSPORT_RCCL && !m->has_root())
+        MHIP(m, hipStreamWaitEvent(j.stream, k->ev_sent[s], 0));
+    return RT_OK;
+}
+
+void worker_main(rt_multi* m, Rank* k) {
+    uint64_t seen = 0;
+    for (;;) {
+        // spin briefly (a frame loop posts every few tens of microseconds), then sleep
+        uint64_t p = k->posted.load(std::memory_order_acquire);
+        for (int it = 0; p == seen && it < 4096; it++) {
+            std::this_thread::yield();
+            p = k->posted.load(std::memory_order_acquire);
+        }
+        if (p == seen) {
+            std::unique_lock<std::mutex> lk(k->mu);
+            k->cv.wait(lk, [&] { return k->quit || k->posted.load(std::memory_order_acquire) != seen; });
+            if (k->quit) return;
+            p = k->posted.load(std::memory_order_acquire);
+        }
+        seen = p;
+        k->status = enqueue_rank(m, k, k->job);
+        k->finished.store(seen, std::memory_order_release);
+    }
+}
+
+void destroy_rank(Rank* k) {
+    if (k->th.joinable()) {
+        {
+            std::lock_guard<std::mutex> lk(k->mu);
+            k->quit = true;
+        }
+        k->cv.notify_one();
+        k->th.join();
+    }
+    DevGuard dg(k->device);
+    if (k->render_stream) (void)hipStreamSynchronize(k->render_stream);
+    if (k->comm_stream) (void)hipStreamSynchronize(k->comm_stream);
+    if (k->comm) (void)ncclCommDestroy(k->comm);
+    for (auto& b : k->band)
+        if (b) (void)hipFree(b);
+    for (int s = 0; s < RT_MULTI_SLOTS; s++) {
+        if (k->ev_rendered[s]) (void)hipEventDestroy(k->ev_rendered[s]);
+        if (k->ev_sent[s]) (void)hipEventDestroy(k->ev_sent[s]);
+    }
+    if (k->ev_done) (void)hipEventDestroy(k->ev_done);
+    if (k->render_stream) (void)hipStreamDestroy(k->render_stream);
+    if (k->comm_stream) (void)hipStreamDestroy(k->comm_stream);
+    if (k->ctx) (void)rt_ctx_destroy(k->ctx);
+    delete k;
+}
+
+int check_args(const rt_multi* m, const rt_camera* cam, int32_t depth, int32_t precision,
+               int32_t out_format) {
+    if (!m || !cam) return RT_ERR_INVALID_ARG;
+    if (cam->width < 0 || cam->height < 0 || depth < 0) return RT_ERR_INVALID_ARG;
+    if (depth > rt_max_depth()) return RT_ERR_UNSUPPORTED;
+    if (precision < RT_PREC_F64 || precision > RT_PREC_PATH64) return RT_ERR_INVALID_ARG;
+    if (bpp(out_format) == 0) return RT_ERR_INVALID_ARG;
+    return RT_OK;
+}
+
+/* One frame of rt_multi_render_device (arguments already checked). */
+int render_frame(rt_multi* m, const rt_camera* cam, int32_t depth, int32_t precision, uint32_t flags,
+                 int32_t out_format, void* d_frame, void* stream) {
+    const int slot = (int)(m->frame % RT_MULTI_SLOTS);
+    Job j;
+    j.cam = cam;
+    j.depth = depth;
+    j.precision = precision;
+    j.flags = flags;
+    j.out_format = out_format;
+    j.d_frame = static_cast<char*>(d_frame);
+    j.slot = slot;
+    Rank* root = m->has_root() ? m->r[0] : nullptr;
+    if (root) {
+        if (!d_frame && (size_t)cam->width * cam->height > 0) return RT_ERR_INVALID_ARG;
+        DevGuard dg(root->device);
+        MHIP(m, dg.err);
+        j.stream = stream ? static_cast<hipStream_t>(stream) : root->render_stream;
+        j.ev_in = m->ev_in[slot];
+        MHIP(m, hipEventRecord(j.ev_in, j.stream));
+    } else {
+        j.stream = static_cast<hipStream_t>(stream);
+    }
+    // the extra local ranks on their worker threads, the first on this thread
+    for (int L = 1; L < m->nlocal; L++) {
+        Rank* k = m->r[L];
+        {
+            std::lock_guard<std::mutex> lk(k->mu);
+            k->job = j;
+            k->job.stream = nullptr;  // only the process's first rank sees the caller's stream
+            k->posted.store(m->frame + 1, std::memory_order_release);
+        }
+        k->cv.notify_one();
+    }
+    int st = enqueue_rank(m, m->r[0], j);
+    for (int L = 1; L < m->nlocal; L++) {
+        Rank* k = m->r[L];
+        while (k->finished.load(std::memory_order_acquire) != m->frame + 1) std::this_thread::yield();
+        if (st == RT_OK && k->status != RT_OK) st = k->status;
+    }
+    m->frame++;
+    if (st != RT_OK) return st;
+    if (root && m->nranks > 1) {
+        // the caller's stream sees the complete frame
+        DevGuard dg(root->device);
+        MHIP(m, dg.err);
+        if (m->transport == RT_TRANSPORT_RCCL) {
+            MHIP(m, hipStreamWaitEvent(j.stream, root->ev_done, 0));
+        } else {
+            for (int L = 1; L < m->nlocal; L++) MHIP(m, hipStreamWaitEvent(j.stream, m->r[L]->ev_sent[slot], 0));
+        }
+    }
+    return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_multi_unique_id(uint8_t id[RT_MULTI_ID_BYTES]) {
+    if (!id) return RT_ERR_INVALID_ARG;
+    ncclUniqueId u;
+    if (ncclGetUniqueId(&u) != ncclSuccess) return RT_ERR_COMM;
+    static_assert(sizeof u == RT_MULTI_ID_BYTES, "ncclUniqueId size");
+    std::memcpy(id, &u, sizeof u);
+    return RT_OK;
+}
+
+const char* rt_multi_last_error(const rt_multi* m) { return m ? m->last_err : ""; }
+
+int rt_multi_create(const int32_t* devices, int32_t nlocal, int32_t nranks, int32_t first_rank,
+                    const uint8_t* unique_id, int32_t transport, rt_multi** out) {
+    if (!out) return RT_ERR_INVALID_ARG;
+    *out = nullptr;
+    if (!devices || nlocal <= 0 || nranks <= 0 || first_rank < 0 || first_rank + nlocal > nranks)
+        return RT_ERR_INVALID_ARG;
+    if (transport != RT_TRANSPORT_RCCL && transport != RT_TRANSPORT_COPY) return RT_ERR_INVALID_ARG;
+    const bool one_process = nlocal == nranks;
+    if (!one_process && (!unique_id || transport == RT_TRANSPORT_COPY))
+        return transport == RT_TRANSPORT_COPY ? RT_ERR_UNSUPPORTED : RT_ERR_INVALID_ARG;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return RT_ERR_NO_DEVICE;
+    for (int L = 0; L < nlocal; L++)
+        if (devices[L] < 0 || devices[L] >= ndev) return RT_ERR_NO_DEVICE;
+    if (transport == RT_TRANSPORT_RCCL)
+        for (int a = 0; a < nlocal; a++)
+            for (int b = a + 1; b < nlocal; b++)
+                if (devices[a] == devices[b]) return RT_ERR_UNSUPPORTED;  // RCCL: one rank per GPU
+
+    rt_multi* m = new (std::nothrow) rt_multi();
+    if (!m) return RT_ERR_OUT_OF_MEMORY;
+    m->nranks = nranks;
+    m->nlocal = nlocal;
+    m->first_rank = first_rank;
+    m->transport = transport;
+    int st = RT_OK;
+    auto fail = [&](int s) {
+        st = s;
+        return s;
+    };
+    for (int L = 0; L < nlocal && st == RT_OK; L++) {
+        Rank* k = new (std::nothrow) Rank();
+        if (!k) {
+            fail(RT_ERR_OUT_OF_MEMORY);
+            break;
+        }
+        m->r.push_back(k);
+        k->rank = first_rank + L;
+        k->device = devices[L];
+        int cs = rt_ctx_create(k->device, &k->ctx);
+        if (cs != RT_OK) {
+            fail(cs);
+            break;
+        }
+        DevGuard dg(k->device);
+        hipError_t e = dg.err;
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&k->render_stream, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&k->comm_stream, hipStreamNonBlocking);
+        for (int s = 0; s < RT_MULTI_SLOTS && e == hipSuccess; s++) {
+            e = hipEventCreateWithFlags(&k->ev_rendered[s], hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&k->ev_sent[s], hipEventDisableTiming);
+            // recorded once, so the first wait on a slot (no send yet) is already satisfied
+            if (e == hipSuccess) e = hipEventRecord(k->ev_sent[s], k->comm_stream);
+        }
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&k->ev_done, hipEventDisableTiming);
+        if (e != hipSuccess) fail(hip_err(m, e, "rank streams/events"));
+    }
+    if (st == RT_OK && m->has_root()) {
+        DevGuard dg(m->r[0]->device);
+        hipError_t e = dg.err;
+        for (int s = 0; s < RT_MULTI_SLOTS && e == hipSuccess; s++)
+            e = hipEventCreateWithFlags(&m->ev_in[s], hipEventDisableTiming);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&m->host_stream, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreate(&m->ev0);
+        if (e == hipSuccess) e = hipEventCreate(&m->ev1);
+        if (e != hipSuccess) fail(hip_err(m, e, "root streams/events"));
+        if (st == RT_OK && transport == RT_TRANSPORT_COPY) {
+            // direct xGMI peer copies where the devices allow it (else the runtime stages)
+            for (int L = 1; L < nlocal; L++) {
+                const int d = m->r[L]->device, d0 = m->r[0]->device;
+                int can = 0;
+                if (d != d0 && hipDeviceCanAccessPeer(&can, d, d0) == hipSuccess && can) {
+                    DevGuard g2(d);
+                    const hipError_t pe = hipDeviceEnablePeerAccess(d0, 0);
+                    if (pe != hipSuccess && pe != hipErrorPeerAccessAlreadyEnabled)
+                        (void)hipGetLastError();
+                    else if (pe == hipErrorPeerAccessAlreadyEnabled)
+                        (void)hipGetLastError();
+                }
+            }
+        }
+    }
+    if (st == RT_OK && transport == RT_TRANSPORT_RCCL) {
+        ncclUniqueId id;
+        if (one_process && !unique_id) {
+            if (ncclGetUniqueId(&id) != ncclSuccess) fail(nccl_err(m, ncclInternalError, "ncclGetUniqueId"));
+        } else {
+            std::memcpy(&id, unique_id, sizeof id);
+        }
+        if (st == RT_OK) {
+            // one rank per device; several local ranks join inside one group (what
+            // ncclCommInitAll does)
+            ncclResult_t e = nlocal > 1 ? ncclGroupStart() : ncclSuccess;
+            for (int L = 0; L < nlocal && e == ncclSuccess; L++) {
+                DevGuard dg(m->r[L]->device);
+                e = ncclCommInitRank(&m->r[L]->comm, nranks, id, m->r[L]->rank);
+            }
+            const ncclResult_t e2 = nlocal > 1 ? ncclGroupEnd() : ncclSuccess;
+            if (e != ncclSuccess || e2 != ncclSuccess)
+                fail(nccl_err(m, e != ncclSuccess ? e : e2, "ncclCommInitRank"));
+        }
+    }
+    if (st == RT_OK) {
+        for (int L = 1; L < nlocal; L++) {
+            Rank* k = m->r[L];
+            try {
+                k->th = std::thread(worker_main, m, k);
+            } catch (...) {
+                fail(RT_ERR_OUT_OF_MEMORY);
+                break;
+            }
+        }
+    }
+    if (st != RT_OK) {
+        std::fprintf(stderr, "rt_multi_create: %s %s\n", rt_strerror(st), m->last_err);
+        rt_multi_destroy(m);
+        return st;
+    }
+    *out = m;
+    return RT_OK;
+}
+
+int rt_multi_destroy(rt_multi* m) {
+    if (!m) return RT_ERR_INVALID_ARG;
+    for (Rank* k : m->r) destroy_rank(k);
+    m->r.clear();
+    // the root's device objects (every rank has been synchronised above)
+    for (auto& e : m->ev_in)
+        if (e) (void)hipEventDestroy(e);
+    if (m->ev0) (void)hipEventDestroy(m->ev0);
+    if (m->ev1) (void)hipEventDestroy(m->ev1);
+    if (m->host_stream) (void)hipStreamDestroy(m->host_stream);
+    if (m->d_frame) (void)hipFree(m->d_frame);
+    delete m;
+    return RT_OK;
+}
+
+int rt_multi_set_scene(rt_multi* m, const rt_prim* prims, int32_t n) {
+    if (!m) return RT_ERR_INVALID_ARG;
+    for (Rank* k : m->r) {
+        const int st = rt_set_scene(k->ctx, prims, n);
+        if (st != RT_OK) return ctx_err(m, k, st, "rt_set_scene");
+    }
+    return RT_OK;
+}
+
+int rt_multi_set_option(rt_multi* m, int32_t option, int64_t value) {
+    if (!m) return RT_ERR_INVALID_ARG;
+    for (Rank* k : m->r) {
+        const int st = rt_set_option(k->ctx, option, value);
+        if (st != RT_OK) return ctx_err(m, k, st, "rt_set_option");
+    }
+    return RT_OK;
+}
+
+int rt_multi_render_device(rt_multi* m, const rt_camera* cam, int32_t depth, int32_t precision,
+                           uint32_t flags, int32_t out_format, void* d_frame, void* stream) {
+    const int st = check_args(m, cam, depth, precision, out_format);
+    if (st != RT_OK) return st;
+    return render_frame(m, cam, depth, precision, flags, out_format, d_frame, stream);
+}
+
+int rt_multi_render_device_frames(rt_multi* m, const rt_camera* cams, int32_t ncams,
+                                  int32_t depth, int32_t precision, uint32_t flags,
+                                  int32_t out_format, void* const* d_frames, int32_t nbufs,
+                                  void* const* streams, int32_t nstreams, int32_t nframes) {
+    if (!m || !cams || ncams <= 0 || nframes < 0 || nbufs < 0 || nstreams < 0 ||
+        (nbufs > 0 && !d_frames) || (nstreams > 0 && !streams))
+        return RT_ERR_INVALID_ARG;
+    if (m->has_root() && nbufs == 0) return RT_ERR_INVALID_ARG;
+    for (int32_t f = 0; f < nframes; f++) {
+        const rt_camera* cam = &cams[f % ncams];
+        int st = check_args(m, cam, depth, precision, out_format);
+        if (st != RT_OK) return st;
+        st = render_frame(m, cam, depth, precision, flags, out_format,
+                          nbufs > 0 ? d_frames[f % nbufs] : nullptr,
+                          nstreams > 0 ? streams[f % nstreams] : nullptr);
+        if (st != RT_OK) return st;
+    }
+    return RT_OK;
+}
+
+int rt_multi_render(rt_multi* m, const rt_camera* cam, int32_t depth, int32_t precision,
+                    uint32_t flags, int32_t out_format, void* out, rt_stats* stats) {
+    int st = check_args(m, cam, depth, precision, out_format);
+    if (st != RT_OK) return st;
+    const size_t bytes = (size_t)cam->width * cam->height * bpp(out_format);
+    if (!m->has_root()) {
+        st = render_frame(m, cam, depth, precision, flags, out_format, nullptr, nullptr);
+        if (st != RT_OK) return st;
+        if (stats) *stats = rt_stats{0.0, 0};
+        return rt_multi_sync(m);
+    }
+    if (!out && bytes > 0) return RT_ERR_INVALID_ARG;
+    Rank* root = m->r[0];
+    {
+        DevGuard dg(root->device);
+        MHIP(m, dg.err);
+        if (bytes > m->d_frame_cap) {
+            MHIP(m, hipStreamSynchronize(m->host_stream));
+            if (m->d_frame) MHIP(m, hipFree(m->d_frame));
+            m->d_frame = nullptr;
+            m->d_frame_cap = 0;
+            MHIP(m, hipMalloc(&m->d_frame, bytes));
+            m->d_frame_cap = bytes;
+        }
+        MHIP(m, hipEventRecord(m->ev0, m->host_stream));
+    }
+    st = render_frame(m, cam, depth, precision, flags, out_format, m->d_frame, m->host_stream);
+    if (st != RT_OK) return st;
+    DevGuard dg(root->device);
+    MHIP(m, dg.err);
+    MHIP(m, hipEventRecord(m->ev1, m->host_stream));
+    if (bytes > 0) MHIP(m, hipMemcpyAsync(out, m->d_frame, bytes, hipMemcpyDeviceToHost, m->host_stream));
+    MHIP(m, hipStreamSynchronize(m->host_stream));
+    st = rt_multi_sync(m);
+    if (st != RT_OK) return st;
+    if (stats) {
+        float ms = 0.f;
+        MHIP(m, hipEventElapsedTime(&ms, m->ev0, m->ev1));
+        stats->ms = ms;
+        stats->segments = 0;
+    }
+    return RT_OK;
+}
+
+int rt_multi_sync(rt_multi* m) {
+    if (!m) return RT_ERR_INVALID_ARG;
+    for (Rank* k : m->r) {
+        DevGuard dg(k->device);
+        MHIP(m, dg.err);
+        MHIP(m, hipStreamSynchronize(k->render_stream));
+        MHIP(m, hipStreamSynchronize(k->comm_stream));
+        if (k->comm) {
+            ncclResult_t async = ncclSuccess;
+            MNCCL(m, ncclCommGetAsyncError(k->comm, &async));
+            if (async != ncclSuccess) return nccl_err(m, async, "ncclCommGetAsyncError");
+        }
+    }
+    return RT_OK;
+}
+
+}  // extern "C"

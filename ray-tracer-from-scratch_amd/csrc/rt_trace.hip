@@ -97,9 +97,6 @@
 #ifndef RT_WALL_ORDER      // 1: the primary scan visits walls in the host's per-frame order
 #define RT_WALL_ORDER 1    // (nearest to the camera first) when KParams::wall_order is set
 #endif
-#ifndef RT_WALL_ORDER      // 1: the primary scan visits walls in the host's per-frame order
-#define RT_WALL_ORDER 1    // (nearest to the camera first) when KParams::wall_order is set
-#endif
 #ifndef RT_WALL_PAIRS      // exact wall tests two at a time in one basic block (ILP)
 #define RT_WALL_PAIRS 0    // A/B: +10% at c2 (lost t-skip, +16 VGPRs), off
 #endif
@@ -2214,6 +2211,7 @@ k_trace(KParams p) {
 #ifndef RT_WPE_PAIR
 #define RT_WPE_PAIR 3
 #endif
+#if RT_WAVES_PER_BLOCK == 1 && !RT_TILE_PAIRS  // one-wave 8x8 tiles only (see launch_trace_ns)
 template <bool SUN, int MAXD>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_WPE_PAIR, 8)))
 k_trace_pair(KParams p) {
@@ -2261,6 +2259,7 @@ static hipError_t launch_pair(const KParams& p, dim3 grid, hipStream_t st, hipEv
         go(k_trace_pair<SUN, MAXD_LARGE>);
     return hipGetLastError();
 }
+#endif  // RT_WAVES_PER_BLOCK == 1 && !RT_TILE_PAIRS
 
 template <int PREC, bool SUN, bool INT_EXP, bool CULL, int MAXD>
 static void launch_one(const KParams& p, dim3 grid, hipStream_t st, hipEvent_t done) {
@@ -2320,13 +2319,17 @@ int launch_trace_ns(const KParams& p, int prec, void* stream, void* done_event) 
                     RT_TILE_PAIRS ? (units + 1) / 2 : units);
     hipStream_t st = static_cast<hipStream_t>(stream);
     hipEvent_t done = static_cast<hipEvent_t>(done_event);
-    if (p.pairs && prec == PREC_PATH64 && !p.wave_cull && BLOCK == 64 && !RT_TILE_PAIRS) {
+    // two pixels per lane exist only in one-wave (8x8 tile) builds: the pair kernel is not
+    // instantiated for RT_WAVES_PER_BLOCK > 1 or RT_TILE_PAIRS (RT_OPT_PIXEL_PAIRS ignored)
+#if RT_WAVES_PER_BLOCK == 1 && !RT_TILE_PAIRS
+    if (p.pairs && prec == PREC_PATH64 && !p.wave_cull) {
         // 16x8 pixels per wave: half the tile columns per dispatch unit
         const int gxp = (((p.W + TILE_W - 1) / TILE_W) + 1) >> 1;
         const dim3 gp((gxp + (1 << ul) - 1) >> ul, units);
         return (int)((p.flags & FLAG_SUN) ? launch_pair<true>(p, gp, st, done)
                                           : launch_pair<false>(p, gp, st, done));
     }
+#endif
     switch (prec) {
         case PREC_F64: return (int)launch_prec<PREC_F64>(p, grid, st, done);
         case PREC_F32: return (int)launch_prec<PREC_F32>(p, grid, st, done);

@@ -18,7 +18,8 @@
  *             path64|f32] [--scene default|synthetic:S,W[,seed]] [--ppm file] [--gpu-surface]
  *
  * --gpu-surface replaces rt_scene + the host packing loop by one rt_render with the
- * kernel's RGBA8 epilogue (clamp, truncate v*255: the in-range behaviour of main.cpp:345).
+ * kernel's RT_OUT_RGBA8_WRAP epilogue: the same bytes main.cpp:345 produces, highlights
+ * above 1.0 wrapping modulo 256 as the reference's x86-64 build does.
  */
 #include <chrono>
 #include <cmath>
@@ -126,11 +127,15 @@ void build_scene(const std::string& spec, std::vector<std::unique_ptr<SceneGeome
     }
 }
 
-inline uint8_t to_u8(double v) {  // SDL_MapRGB's Uint8 argument from val*255 (in range)
-    v *= 255;
-    v = v > 0 ? v : 0;
-    v = v < 255 ? v : 255;
-    return (uint8_t)v;
+/* SDL_MapRGB's Uint8 argument from val*255 (main.cpp:345): the double converts implicitly,
+ * which the reference's x86-64 build does with cvttsd2si (truncate to int32; NaN and values
+ * outside the int32 range give INT32_MIN) and the low byte — in-range values truncate,
+ * highlights above 1.0 wrap modulo 256 (1.084 displays as 20).  Written without the
+ * undefined conversion so any compiler gives those bytes. */
+inline uint8_t to_u8(double v) {
+    const double t = v * 255;
+    const int32_t i = (t > -2147483649.0 && t < 2147483648.0) ? (int32_t)t : INT32_MIN;
+    return (uint8_t)((uint32_t)i & 0xffu);
 }
 
 }  // namespace
@@ -196,7 +201,7 @@ int main(int argc, char** argv) {
             }
             c.width = W;
             c.height = H;
-            if (rt_render(ctx, &c, 0, H, a.depth, a.precision, 0, RT_OUT_RGBA8, surface.data(), 0,
+            if (rt_render(ctx, &c, 0, H, a.depth, a.precision, 0, RT_OUT_RGBA8_WRAP, surface.data(), 0,
                           nullptr) != RT_OK) {
                 std::fprintf(stderr, "rt_render failed: %s\n", rt_last_hip_error(ctx));
                 return 1;

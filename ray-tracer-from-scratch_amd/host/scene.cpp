@@ -9,8 +9,18 @@
  */
 #include <cfloat>
 #include <cmath>
+#include <stdexcept>
 
 #include "../../include/rt/scene.h"
+
+/* A primitive type the kernels do not implement (a SceneGeometry subclass written against
+ * the reference's scene.h:51-60, which has intersect() only): rt_scene reports it instead
+ * of rendering something else. */
+void SceneGeometry::pack(rt_prim*) const {
+    throw std::invalid_argument(
+        "rt_scene: unsupported primitive: this SceneGeometry subclass has no GPU record "
+        "(the kernels implement Sphere and Wall; override pack())");
+}
 
 void SceneGeometry::pack_material(rt_prim* out) const {
     out->mat.color[0] = mat.color.x;

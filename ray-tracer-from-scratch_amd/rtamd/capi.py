@@ -26,6 +26,12 @@ RT_ERR_OUT_OF_MEMORY = 4
 RT_ERR_NO_SCENE = 5
 RT_ERR_UNSUPPORTED = 6
 RT_ERR_OUT_OF_RANGE = 7
+RT_ERR_COMM = 8
+
+RT_TRANSPORT_RCCL = 0
+RT_TRANSPORT_COPY = 1
+RT_MULTI_ID_BYTES = 128
+RT_MULTI_SLOTS = 2
 
 RT_PRIM_SPHERE = 0
 RT_PRIM_WALL = 1
@@ -129,6 +135,25 @@ SIGNATURES = [
     ("rt_selftest", C.c_int, [C.c_void_p, C.c_int32, C.c_uint64, C.c_uint64,
                               C.POINTER(C.c_uint64)]),
     ("rt_set_row_order", C.c_int, [C.c_void_p, C.POINTER(C.c_int16), C.c_int32]),
+    # multi-GPU frame operator
+    ("rt_multi_unique_id", C.c_int, [C.POINTER(C.c_uint8)]),
+    ("rt_multi_create", C.c_int,
+     [C.POINTER(C.c_int32), C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_uint8), C.c_int32,
+      C.POINTER(C.c_void_p)]),
+    ("rt_multi_destroy", C.c_int, [C.c_void_p]),
+    ("rt_multi_last_error", C.c_char_p, [C.c_void_p]),
+    ("rt_multi_set_scene", C.c_int, [C.c_void_p, C.POINTER(rt_prim), C.c_int32]),
+    ("rt_multi_set_option", C.c_int, [C.c_void_p, C.c_int32, C.c_int64]),
+    ("rt_multi_render_device", C.c_int,
+     [C.c_void_p, C.POINTER(rt_camera), C.c_int32, C.c_int32, C.c_uint32, C.c_int32, C.c_void_p,
+      C.c_void_p]),
+    ("rt_multi_render_device_frames", C.c_int,
+     [C.c_void_p, C.POINTER(rt_camera), C.c_int32, C.c_int32, C.c_int32, C.c_uint32, C.c_int32,
+      C.POINTER(C.c_void_p), C.c_int32, C.POINTER(C.c_void_p), C.c_int32, C.c_int32]),
+    ("rt_multi_render", C.c_int,
+     [C.c_void_p, C.POINTER(rt_camera), C.c_int32, C.c_int32, C.c_uint32, C.c_int32, C.c_void_p,
+      C.POINTER(rt_stats)]),
+    ("rt_multi_sync", C.c_int, [C.c_void_p]),
 ]
 
 _lib = None
@@ -310,3 +335,106 @@ class Renderer:
         check(self.lib.rt_render_device_frames(self.ctx, ca, len(cams), row0, nrows, depth,
                                                precision, flags, out_format, outs, len(d_outs),
                                                sts, len(streams), nframes), self.ctx)
+
+
+def multi_unique_id() -> bytes:
+    """rt_multi_unique_id: a communicator id to share with every process (one-process-per-GPU
+    model of rt_multi_create)."""
+    lib = load()
+    buf = (C.c_uint8 * RT_MULTI_ID_BYTES)()
+    check(lib.rt_multi_unique_id(buf))
+    return bytes(buf)
+
+
+class MultiRenderer:
+    """One rt_multi: ONE frame split into row bands over `nranks` GPUs and gathered into the
+    frame buffer of rank 0 (include/rt_capi.h "multi-GPU frame operator").
+
+    MultiRenderer([0, 1, 2, 3])                         one process drives 4 GPUs (RCCL)
+    MultiRenderer([0, 0, 0], transport=RT_TRANSPORT_COPY)  3 ranks on one GPU, peer copies
+    MultiRenderer([local], nranks=N, first_rank=rank, unique_id=id)   one process per GPU
+    """
+
+    def __init__(self, devices, nranks: int | None = None, first_rank: int = 0,
+                 unique_id: bytes | None = None, transport: int = RT_TRANSPORT_RCCL):
+        self.lib = load()
+        devs = list(devices)
+        self.nranks = len(devs) if nranks is None else int(nranks)
+        self.first_rank = int(first_rank)
+        self.devices = devs
+        arr = (C.c_int32 * len(devs))(*devs)
+        uid = None
+        if unique_id is not None:
+            uid = (C.c_uint8 * RT_MULTI_ID_BYTES)(*unique_id)
+        h = C.c_void_p()
+        check(self.lib.rt_multi_create(arr, len(devs), self.nranks, self.first_rank, uid,
+                                       int(transport), C.byref(h)))
+        self.m = h
+
+    def _check(self, st: int) -> None:
+        if st != RT_OK:
+            raise RTError(st, (self.lib.rt_multi_last_error(self.m) or b"").decode())
+
+    @property
+    def has_root(self) -> bool:
+        return self.first_rank == 0
+
+    def close(self):
+        if getattr(self, "m", None):
+            self.lib.rt_multi_destroy(self.m)
+            self.m = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_scene(self, prims) -> None:
+        arr = (rt_prim * max(1, len(prims)))(*prims)
+        self._prims = arr
+        self._check(self.lib.rt_multi_set_scene(self.m, arr, len(prims)))
+
+    def set_option(self, option: int, value: int) -> None:
+        self._check(self.lib.rt_multi_set_option(self.m, option, value))
+
+    def render(self, cam: rt_camera, depth: int, precision: int = RT_PREC_PATH64, flags: int = 0,
+               out_format: int = RT_OUT_RGB_F32):
+        """Synchronous: (frame on the root's process else None, stats)."""
+        st = rt_stats()
+        out = None
+        ptr = None
+        if self.has_root:
+            dt, shape = out_dtype_shape(out_format, cam.height, cam.width)
+            out = np.empty(shape, dtype=dt)
+            ptr = out.ctypes.data_as(C.c_void_p)
+        self._check(self.lib.rt_multi_render(self.m, C.byref(cam), depth, precision, flags,
+                                             out_format, ptr, C.byref(st)))
+        return out, st
+
+    def render_device(self, cam: rt_camera, depth: int, d_frame: int, precision: int = RT_PREC_PATH64,
+                      flags: int = 0, out_format: int = RT_OUT_RGB_F32, stream: int = 0) -> None:
+        self._check(self.lib.rt_multi_render_device(self.m, C.byref(cam), depth, precision, flags,
+                                                    out_format, C.c_void_p(d_frame or None),
+                                                    C.c_void_p(stream or None)))
+
+    def render_device_frames(self, cams, depth: int, d_frames, precision: int = RT_PREC_PATH64,
+                             flags: int = 0, out_format: int = RT_OUT_RGB_F32, streams=(),
+                             nframes: int = 1) -> None:
+        cams = list(cams)
+        ca = (rt_camera * len(cams))(*cams)
+        d_frames = list(d_frames)
+        outs = (C.c_void_p * max(1, len(d_frames)))(*[C.c_void_p(o or None) for o in d_frames])
+        sts = (C.c_void_p * max(1, len(streams)))(*[C.c_void_p(x or None) for x in streams])
+        self._check(self.lib.rt_multi_render_device_frames(
+            self.m, ca, len(cams), depth, precision, flags, out_format, outs, len(d_frames), sts,
+            len(streams), nframes))
+
+    def sync(self) -> None:
+        self._check(self.lib.rt_multi_sync(self.m))

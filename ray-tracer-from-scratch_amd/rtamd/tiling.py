@@ -121,17 +121,19 @@ def render_tiled(renderer: "capi.Renderer", cam, depth: int, precision: int = ca
     tdtype = {"float32": torch.float32, "float64": torch.float64, "uint8": torch.uint8}[
         dt_np.__name__]
     dev = torch.device("cuda", torch.cuda.current_device())
-    st = stream or torch.cuda.current_stream(dev)
+    # never the legacy default stream (handle 0): the C-ABI maps a NULL stream to the ctx's
+    # own non-blocking stream, which nothing on the torch side would be ordered with
+    st = stream if stream is not None and stream.cuda_stream != 0 else torch.cuda.Stream(dev)
 
     def band(row0, nrows, out):
         cur = torch.cuda.current_stream(dev)
         if st != cur:
-            st.wait_stream(cur)  # the band buffer was produced on the current stream
+            st.wait_stream(cur)  # the band buffer was produced (zeroed) on the current stream
         renderer.render_device(cam, depth, out.data_ptr(), precision, flags, out_format,
                                row0=row0, nrows=nrows, stream=st.cuda_stream)
         if st != cur:
             # ProcessGroupNCCL orders the gather after the CURRENT stream only: make it wait
-            # for the band's kernel on the caller's stream
+            # for the band's kernel on the render stream
             cur.wait_stream(st)
 
     return gather_frame(band, cam.height, cam.width, shape[-1], tdtype, dev, group, dst)

@@ -5,6 +5,11 @@
 //   dropin_main render W H [depth]  rt_scene on the GPU; writes H*W*3 doubles to stdout
 //   dropin_main throws W H          [W][H]-allocated framebuffer (main.cpp:243): prints 1 if
 //                                   rt_scene throws std::out_of_range
+//   dropin_main plugin              a SceneGeometry subclass written against the reference's
+//                                   interface (intersect only) compiles; rt_scene prints 1 if
+//                                   it throws std::invalid_argument (no device needed)
+//   dropin_main render_multi W H N [transport]  rt_scene row-tiled over N ranks on device 0
+//                                   (RtSceneOptions::devices = {0 x N}); same output as render
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -21,6 +26,13 @@ static std::vector<std::unique_ptr<SceneGeometry>> default_scene() {
     scene.push_back(std::make_unique<Wall>(Material(RGB(0, 1, 0)), point3(3.0, -3, 0), vec3(0, 1, 0), 2, 2));
     return scene;
 }
+
+// a primitive plugin as a reference user would write it (scene.h:51-60: intersect only)
+class Disc : public SceneGeometry {
+public:
+    Disc() : SceneGeometry(Material(RGB(1, 0, 0))) {}
+    Collision intersect(ray) const override { return Collision(-1, vec3(0, 0, 0), false, -1); }
+};
 
 static Camera make_camera(int w, int h) {
     Camera cam;
@@ -70,6 +82,39 @@ int main(int argc, char** argv) {
         auto u = cam.init();
         std::vector<std::vector<RGB>> frame_buffer(H, std::vector<RGB>(W, RGB(0, 0, 0)));
         rt_scene(u, scene, cam, frame_buffer);
+        for (int i = 0; i < H; i++)
+            for (int j = 0; j < W; j++) {
+                const double v[3] = {frame_buffer[i][j].x, frame_buffer[i][j].y, frame_buffer[i][j].z};
+                std::fwrite(v, sizeof v, 1, stdout);
+            }
+        return 0;
+    }
+    if (mode == "plugin") {
+        auto scene = default_scene();
+        scene.push_back(std::make_unique<Disc>());
+        Camera cam = make_camera(32, 32);
+        auto u = cam.init();
+        std::vector<std::vector<RGB>> frame_buffer(32, std::vector<RGB>(32, RGB(0, 0, 0)));
+        try {
+            rt_scene(u, scene, cam, frame_buffer);
+        } catch (const std::invalid_argument& e) {
+            std::printf("1 %s\n", e.what());
+            return 0;
+        }
+        std::printf("0\n");
+        return 0;
+    }
+    if (mode == "render_multi" && argc >= 5) {
+        const int W = std::atoi(argv[2]), H = std::atoi(argv[3]), N = std::atoi(argv[4]);
+        RtSceneOptions o = rt_scene_get_options();
+        o.devices.assign(N, 0);
+        o.transport = argc >= 6 ? std::atoi(argv[5]) : RT_TRANSPORT_COPY;
+        rt_scene_set_options(o);
+        auto scene = default_scene();
+        Camera cam = make_camera(W, H);
+        auto u = cam.init();
+        std::vector<std::vector<RGB>> frame_buffer(H, std::vector<RGB>(W, RGB(0, 0, 0)));
+        for (int rep = 0; rep < 2; rep++) rt_scene(u, scene, cam, frame_buffer);
         for (int i = 0; i < H; i++)
             for (int j = 0; j < W; j++) {
                 const double v[3] = {frame_buffer[i][j].x, frame_buffer[i][j].y, frame_buffer[i][j].z};

@@ -8,7 +8,7 @@ import re
 import numpy as np
 import pytest
 
-from conftest import REPO
+from conftest import REPO, has_gpu
 from rtamd import capi, scenes
 
 
@@ -74,7 +74,8 @@ def test_formats_and_status_strings():
     assert lib.rt_out_bytes_per_pixel(99) == 0
     assert lib.rt_strerror(capi.RT_OK) == b"ok"
     assert lib.rt_strerror(capi.RT_ERR_OUT_OF_RANGE) == b"row band out of range"
-    assert lib.rt_capi_version() == 1
+    assert lib.rt_capi_version() == 2
+    assert lib.rt_strerror(capi.RT_ERR_COMM) == b"RCCL communication error"
     assert lib.rt_max_depth() >= 10   # rt_scene's default depth (main.cpp:89)
 
 
@@ -110,3 +111,31 @@ def test_config_cameras():
     for name, cfg in scenes.CONFIGS.items():
         cam = capi.camera_init(**scenes.camera_args(cfg.width, cfg.height))
         assert (cam.width, cam.height) == (cfg.width, cfg.height), name
+
+
+def test_multi_args_rejected_without_device():
+    """rt_multi_* argument checks happen before any device call."""
+    lib = capi.load()
+    h = C.c_void_p()
+    devs = (C.c_int32 * 2)(0, 1)
+    assert lib.rt_multi_create(devs, 2, 2, 0, None, 0, None) == capi.RT_ERR_INVALID_ARG
+    assert lib.rt_multi_create(None, 1, 1, 0, None, 0, C.byref(h)) == capi.RT_ERR_INVALID_ARG
+    assert lib.rt_multi_create(devs, 0, 1, 0, None, 0, C.byref(h)) == capi.RT_ERR_INVALID_ARG
+    assert lib.rt_multi_create(devs, 2, 1, 0, None, 0, C.byref(h)) == capi.RT_ERR_INVALID_ARG
+    assert lib.rt_multi_create(devs, 1, 2, 0, None, 7, C.byref(h)) == capi.RT_ERR_INVALID_ARG
+    # one process per GPU needs the shared communicator id; COPY is one process only
+    assert lib.rt_multi_create(devs, 1, 2, 1, None, 0, C.byref(h)) == capi.RT_ERR_INVALID_ARG
+    uid = (C.c_uint8 * capi.RT_MULTI_ID_BYTES)()
+    assert lib.rt_multi_create(devs, 1, 2, 1, uid, 1, C.byref(h)) == capi.RT_ERR_UNSUPPORTED
+    if not has_gpu():
+        assert lib.rt_multi_create(devs, 1, 1, 0, None, 0, C.byref(h)) == capi.RT_ERR_NO_DEVICE
+    assert lib.rt_multi_destroy(None) == capi.RT_ERR_INVALID_ARG
+    assert lib.rt_multi_set_scene(None, None, 0) == capi.RT_ERR_INVALID_ARG
+    assert lib.rt_multi_set_option(None, 1, 1) == capi.RT_ERR_INVALID_ARG
+    assert lib.rt_multi_sync(None) == capi.RT_ERR_INVALID_ARG
+    cam = capi.rt_camera()
+    assert lib.rt_multi_render(None, C.byref(cam), 0, 0, 0, 0, None, None) == capi.RT_ERR_INVALID_ARG
+    assert lib.rt_multi_render_device(None, C.byref(cam), 0, 0, 0, 0, None, None) == \
+        capi.RT_ERR_INVALID_ARG
+    assert lib.rt_multi_unique_id(None) == capi.RT_ERR_INVALID_ARG
+    assert lib.rt_multi_last_error(None) == b""

@@ -52,3 +52,26 @@ def test_rt_scene_dropin_matches_reference(dropin, golden_frames):
     out = subprocess.run([dropin, "throws", "64", "48"], capture_output=True, text=True,
                          check=True).stdout
     assert out.strip() == "1"                       # main.cpp:243's [W][H] buffer throws
+
+
+def test_reference_style_plugin_compiles_and_is_reported(dropin):
+    """A SceneGeometry subclass written against the reference's interface (scene.h:51-60:
+    intersect only) compiles against include/rt/scene.h; rt_scene rejects it with
+    std::invalid_argument before any device work (so this runs on the CPU)."""
+    out = subprocess.run([dropin, "plugin"], capture_output=True, text=True, check=True).stdout
+    assert out.startswith("1 ") and "unsupported primitive" in out, out
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not has_gpu(), reason="needs a HIP device")
+@pytest.mark.parametrize("n,transport", [(1, 0), (3, 1), (8, 1)])
+def test_rt_scene_row_tiled_over_devices(dropin, golden_frames, n, transport):
+    """RtSceneOptions::devices: the C++ drop-in renders every frame row-tiled over the listed
+    ranks (rt_multi; RCCL for one rank, peer copies for several ranks on this box's one GPU)
+    — the reference's own depth-10 frame within 1e-12, bitwise the one-GPU drop-in."""
+    raw = subprocess.run([dropin, "render_multi", "48", "48", str(n), str(transport)],
+                         capture_output=True, check=True).stdout
+    img = np.frombuffer(raw, dtype=np.float64).reshape(48, 48, 3)
+    assert np.abs(img - golden_frames["default__48x48__d10"]).max() <= 1e-12
+    one = subprocess.run([dropin, "render", "48", "48"], capture_output=True, check=True).stdout
+    assert raw == one

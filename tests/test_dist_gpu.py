@@ -50,13 +50,18 @@ def _worker(rank, world, port, w, h, depth, fmt, q):
         rend = capi.Renderer(0)
         rend.set_scene(scenes.to_prims(scenes.synthetic_scene(8, 4)))
         ch, dt = (4, torch.uint8) if fmt == capi.RT_OUT_RGBA8 else (3, torch.float32)
-        st = torch.cuda.current_stream(dev)
+        # a non-default render stream: the band waits for the buffer's producer
+        # on the current stream, and the gather (on the current stream) for the band
+        st = torch.cuda.Stream(dev)
         cams = [capi.camera_init(**_frame_args(k, w, h)) for k in range(3)]
         cur = {"k": 0}
 
         def band(row0, nrows, out):
+            cs = torch.cuda.current_stream(dev)
+            st.wait_stream(cs)
             rend.render_device(cams[cur["k"]], depth, out.data_ptr(), capi.RT_PREC_PATH64, 0,
                                fmt, row0=row0, nrows=nrows, stream=st.cuda_stream)
+            cs.wait_stream(st)
 
         frame = tiling.gather_frame(band, h, w, ch, dt, dev)
         if rank == 0:
@@ -80,7 +85,10 @@ def _worker(rank, world, port, w, h, depth, fmt, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,w,h,fmt", [(2, 200, 113, 0), (3, 192, 101, 0), (3, 160, 90, 2)])
+# ragged heights, plus BASELINE config 4's full frame (1920x1080, 8 spheres + 4 walls,
+# depth 4) in both transports: fp32 RGB and the RGBA8 epilogue
+@pytest.mark.parametrize("world,w,h,fmt", [(2, 200, 113, 0), (3, 192, 101, 0), (3, 160, 90, 2),
+                                           (2, 1920, 1080, 0), (3, 1920, 1080, 2)])
 def test_row_tiled_hip_bands_equal_one_frame(world, w, h, fmt):
     from rtamd import capi, scenes
     ctx = mp.get_context("spawn")
@@ -90,7 +98,7 @@ def test_row_tiled_hip_bands_equal_one_frame(world, w, h, fmt):
              for r in range(world)]
     for p in procs:
         p.start()
-    got = [q.get(timeout=110) for _ in range(4)]
+    got = [q.get(timeout=150) for _ in range(4)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0

@@ -401,14 +401,46 @@ def test_path64_sun(rend, oracle):
 
 
 def test_non_integer_specular_exponent(rend, oracle):
-    """A material with a non-integer exponent selects the general-pow kernel variant."""
+    """A material with a non-integer exponent selects the general-pow kernel variants: OCML
+    pow in fp64 (F64/MIXED: the reference's bar), the fp32 pow (`fpow`, exp2(e*log2 x)) in
+    PATH64's colour arithmetic (every pixel within PATH64_TOL, the same ray paths and
+    segment count) and in F32 (its discontinuity bar)."""
     sc = scenes.synthetic_scene(6, 3, seed=3)
     sc[0].mat.specular_exponent = 37.5
     sc[2].mat.specular_exponent = 0.0
-    for prec in (capi.RT_PREC_F64, capi.RT_PREC_MIXED):
-        img, _, cam = render(rend, sc, 64, 36, 5, prec)
-        o64, _, _, sig = oracle.render(scenes.to_prims(sc), cam, 5, want_sig=True)
-        check_f64(img, o64, sig, what=("nonint", prec))
+    sc[4].mat.specular_exponent = 2.25
+    for (w, h) in ((64, 36), (192, 108)):
+        o64 = None
+        for prec in (capi.RT_PREC_F64, capi.RT_PREC_MIXED, capi.RT_PREC_PATH64, capi.RT_PREC_F32):
+            fmt = capi.RT_OUT_RGB_F32 if prec == capi.RT_PREC_F32 else capi.RT_OUT_RGB_F64
+            img, st, cam = render(rend, sc, w, h, 5, prec, fmt=fmt, count_segments=True)
+            if o64 is None:
+                o64, _, segs, sig = oracle.render(scenes.to_prims(sc), cam, 5, want_sig=True)
+            if prec in (capi.RT_PREC_F64, capi.RT_PREC_MIXED):
+                check_f64(img, o64, sig, what=("nonint", prec, w))
+                assert st.segments == segs
+            elif prec == capi.RT_PREC_PATH64:
+                assert st.segments == segs
+                assert np.abs(img - o64).max() <= PATH64_TOL, ("nonint path64", w)
+            else:
+                check_f32(img, o64, sig, 5, ("nonint f32", w))
+
+
+def test_path64_full_size_c5_vs_f64(rend):
+    """BASELINE config 5 (7680x4320, 256 spheres, depth 8) at full size in the bench
+    precision with the sphere-cluster path at its default: PATH64's ray paths are F64's
+    exactly (equal segment counts; the fp32 colour arithmetic is the only difference) and
+    every pixel is within PATH64_TOL of the F64 frame (fp32 output of both)."""
+    cfg = scenes.CONFIGS["c5"]
+    rend.set_scene(scenes.to_prims(cfg.scene()))
+    cam = capi.camera_init(**scenes.camera_args(cfg.width, cfg.height))
+    a, sa = rend.render(cam, cfg.depth, capi.RT_PREC_F64, 0, capi.RT_OUT_RGB_F32,
+                        count_segments=True)
+    b, sb = rend.render(cam, cfg.depth, capi.RT_PREC_PATH64, 0, capi.RT_OUT_RGB_F32,
+                        count_segments=True)
+    assert sa.segments == sb.segments
+    d = np.abs(a - b)
+    assert np.isfinite(d).all() and d.max() <= PATH64_TOL, float(d.max())
 
 
 # ---------------------------------------------------------------- wave cull
@@ -451,7 +483,9 @@ def test_sphere_clusters_are_output_invariant(rend, prec):
     every cluster unpruned), deep bounces."""
     rng = np.random.default_rng(23)
     try:
-        for trial, ns in enumerate((24, 70, 129, 256)):
+        # trial 3: camera far outside the cloud but within the box margin's range (pruned
+        # walk); trial 4: beyond 100x the scene extent (clu_oinf), every cluster unpruned
+        for trial, ns in enumerate((24, 70, 129, 256, 200)):
             sc = scenes.synthetic_scene(ns, int(rng.integers(0, 7)),
                                         seed=int(rng.integers(1 << 30)))
             sph = [o for o in sc if o.kind == capi.RT_PRIM_SPHERE]
@@ -460,10 +494,13 @@ def test_sphere_clusters_are_output_invariant(rend, prec):
                 sc.append(scenes.Sphere(scenes.Material(tuple(rng.uniform(0, 1, 3)), .6),
                                         o.position, o.radius))
             rend.set_scene(scenes.to_prims(sc))
-            far = trial == 3
-            pos = (np.array([-400.0, 30.0, 10.0]) if far else rng.uniform([2, -3, -1], [8, 3, 2]))
+            far = trial >= 3
+            pos = (np.array([-400.0, 30.0, 10.0]) if trial == 3 else
+                   np.array([-5000.0, 40.0, 12.0]) if trial == 4 else
+                   rng.uniform([2, -3, -1], [8, 3, 2]))
             look = np.array([5.0, 0.0, 0.5]) if far else pos + rng.normal(size=3)
-            cam = capi.camera_init(pos, look, (0, 0, -1), 2.0 if far else 100.0, 16 / 9, 160.0)
+            vfov = 2.0 if trial == 3 else 0.15 if trial == 4 else 100.0
+            cam = capi.camera_init(pos, look, (0, 0, -1), vfov, 16 / 9, 160.0)
             depth = 8
             rend.set_option(capi.RT_OPT_WAVE_CULL_MIN_SPHERES, 2**31 - 1)
             ref, rst = rend.render(cam, depth, prec, 0, capi.RT_OUT_RGB_F64, count_segments=True)
@@ -770,12 +807,14 @@ def _read_ppm(path):
     return np.frombuffer(rest, np.uint8).reshape(int(h), int(w), 3)
 
 
-def test_frame_loop_binary(tmp_path, oracle):
+@pytest.mark.parametrize("scene,width", [("default", 64), ("synthetic:16,6,7", 128)])
+def test_frame_loop_binary(tmp_path, oracle, scene, width):
     """bin/rt_frames (host/rt_frames.cpp): main.cpp's loop without SDL — scripted camera
     moves (init() not re-called: stale image_top_left), rt_scene per frame, the
-    SDL_MapRGB packing, and main.cpp's performance log.  The last frame equals the
-    oracle's fp64 frame quantised the same way, with rt_scene (mixed = fp64 path) and with
-    the kernel's RGBA8 epilogue (--gpu-surface)."""
+    SDL_MapRGB(val*255) packing, and main.cpp's performance log.  The last frame's surface
+    equals main.cpp:345's bytes of the oracle's fp64 frame (x86-64 conversion: highlights
+    above 1.0 wrap modulo 256 — the synthetic scene has dozens of them), with rt_scene
+    (mixed = fp64 path) and with the kernel's RT_OUT_RGBA8_WRAP epilogue (--gpu-surface)."""
     import re
     import subprocess
     from conftest import PKG
@@ -783,8 +822,8 @@ def test_frame_loop_binary(tmp_path, oracle):
     outs = {}
     for mode in ("host", "gpu"):
         ppm = str(tmp_path / f"{mode}.ppm")
-        cmd = [exe, "--frames", "3", "--width", "64", "--keys", "wd", "--precision", "mixed",
-               "--ppm", ppm] + (["--gpu-surface"] if mode == "gpu" else [])
+        cmd = [exe, "--frames", "3", "--width", str(width), "--keys", "wd", "--precision", "mixed",
+               "--scene", scene, "--ppm", ppm] + (["--gpu-surface"] if mode == "gpu" else [])
         res = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
         assert res.returncode == 0, res.stderr
         lines = res.stdout.strip().splitlines()
@@ -796,12 +835,21 @@ def test_frame_loop_binary(tmp_path, oracle):
         outs[mode] = _read_ppm(ppm)
     assert np.array_equal(outs["host"], outs["gpu"])
     # expected: frames 'w', 'd', 'w' move the camera (scene.cpp:108-165), init() once
-    cam = capi.camera_init((0, 0, 0), (-1, 0, 0), (0, 0, -1), 90.0, 1.0, 64.0)
+    cam = capi.camera_init((0, 0, 0), (-1, 0, 0), (0, 0, -1), 90.0, 1.0, float(width))
     cam.position[0] = 0.1 + 0.1
     cam.position[1] = 0.1
-    ref64, _, _ = oracle.render(scenes.to_prims(scenes.default_scene()), cam, 10)
-    q = (np.clip(ref64 * 255.0, 0.0, 255.0)).astype(np.uint8)
-    assert np.array_equal(outs["host"], q)
+    if scene == "default":
+        sc = scenes.default_scene()
+    else:
+        ns, nw, seed = (int(v) for v in scene.split(":")[1].split(","))
+        sc = scenes.synthetic_scene(ns, nw, seed=seed)
+    ref64, _, _ = oracle.render(scenes.to_prims(sc), cam, 10)
+    exp = oracle.surface_u8(ref64)
+    t = ref64 * 255.0
+    edge = np.abs(t - np.round(t)) < 1e-9   # fp64 path within 1e-12: only exact boundaries
+    assert ((outs["host"] == exp) | edge).all()
+    if scene != "default":
+        assert int(((ref64 > 1.0) & ~edge).sum()) >= 20   # the wrap is exercised
 
 
 # ---------------------------------------------------------------- multi-GPU path (1 rank)

@@ -1,0 +1,179 @@
+"""The multi-GPU frame operator of the C-ABI (rt_multi_*, include/rt_capi.h) on an MI355X:
+ONE frame split into row bands across ranks, each band rendered by its rank's own rt_ctx,
+gathered into rank 0's frame buffer.  Every gathered frame must be bitwise the one-GPU
+frame (pixels are independent; the reference renders the whole frame on one thread,
+main.cpp:124-139).
+
+One GPU box has one device and RCCL takes one rank per GPU, so:
+  - RCCL is exercised at one rank (the communicator, the caller-stream protocol);
+  - the N-rank orchestration — band offsets, ragged and empty bands, double-buffered band
+    slots, worker threads doing each rank's host work, caller-stream ordering — runs with
+    N ranks on the same GPU through RT_TRANSPORT_COPY (peer copies instead of RCCL
+    send/recv), at BASELINE config 4's full size (1920x1080, 8 spheres + 4 walls, depth 4)
+    for N = 2, 3, 4, 8, fp32 RGB and RGBA8.
+"""
+import numpy as np
+import pytest
+
+from conftest import has_gpu
+from rtamd import capi, scenes
+
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(not has_gpu(), reason="needs a HIP device")]
+
+
+@pytest.fixture(scope="module")
+def rend():
+    r = capi.Renderer(0)
+    yield r
+    r.close()
+
+
+def _cam(w, h, dx=0.0):
+    cam = capi.camera_init(**scenes.camera_args(w, h))
+    cam.position[0] += dx   # Camera::forward without init() (main.cpp:265, scene.cpp:121)
+    return cam
+
+
+def test_single_rank_rccl_equals_render(rend):
+    """RCCL transport with one rank: the frame operator is rt_render of the whole frame."""
+    sc = scenes.synthetic_scene(8, 4)
+    prims = scenes.to_prims(sc)
+    rend.set_scene(prims)
+    with capi.MultiRenderer([0]) as m:
+        m.set_scene(prims)
+        for (w, h) in ((160, 90), (1920, 1080)):
+            cam = _cam(w, h)
+            for prec, fmt in ((capi.RT_PREC_PATH64, capi.RT_OUT_RGB_F32),
+                              (capi.RT_PREC_F64, capi.RT_OUT_RGB_F64),
+                              (capi.RT_PREC_PATH64, capi.RT_OUT_RGBA8)):
+                got, st = m.render(cam, 4, prec, 0, fmt)
+                ref, _ = rend.render(cam, 4, prec, 0, fmt)
+                assert np.array_equal(got.view(np.uint8), ref.view(np.uint8)), (w, prec, fmt)
+                assert st.ms > 0
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 8])
+def test_copy_transport_c4_bands_bitwise(rend, n):
+    """BASELINE config 4 at full size split across n ranks: bitwise the one-GPU frame, in
+    the bench precision and F64, fp32 RGB and the RGBA8 transport."""
+    cfg = scenes.CONFIGS["c2"]   # config 4 = config 2's frame on several GPUs
+    prims = scenes.to_prims(cfg.scene())
+    rend.set_scene(prims)
+    cam = _cam(cfg.width, cfg.height)
+    with capi.MultiRenderer([0] * n, transport=capi.RT_TRANSPORT_COPY) as m:
+        m.set_scene(prims)
+        for prec, fmt in ((capi.RT_PREC_PATH64, capi.RT_OUT_RGB_F32),
+                          (capi.RT_PREC_PATH64, capi.RT_OUT_RGBA8),
+                          (capi.RT_PREC_F64, capi.RT_OUT_RGB_F32)):
+            got, _ = m.render(cam, cfg.depth, prec, 0, fmt)
+            ref, _ = rend.render(cam, cfg.depth, prec, 0, fmt)
+            assert np.array_equal(got.view(np.uint8), ref.view(np.uint8)), (n, prec, fmt)
+
+
+@pytest.mark.parametrize("n,w,h", [(8, 203, 117), (8, 37, 5), (3, 1, 1), (5, 64, 36)])
+def test_ragged_and_empty_bands(rend, n, w, h):
+    """Heights not divisible by the rank count (bands differ by one row) and heights below
+    it (empty bands: nothing rendered or sent)."""
+    prims = scenes.to_prims(scenes.synthetic_scene(8, 4, seed=5))
+    rend.set_scene(prims)
+    cam = _cam(w, h)
+    with capi.MultiRenderer([0] * n, transport=capi.RT_TRANSPORT_COPY) as m:
+        m.set_scene(prims)
+        got, _ = m.render(cam, 5, capi.RT_PREC_F64, 0, capi.RT_OUT_RGB_F64)
+        ref, _ = rend.render(cam, 5, capi.RT_PREC_F64, 0, capi.RT_OUT_RGB_F64)
+        assert np.array_equal(got.view(np.uint64), ref.view(np.uint64))
+
+
+@pytest.mark.parametrize("transport,n", [(capi.RT_TRANSPORT_COPY, 4), (capi.RT_TRANSPORT_RCCL, 1)])
+def test_frames_in_flight_on_caller_streams(rend, transport, n):
+    """The bench's frame loop: many frames of a moving camera enqueued back to back by one
+    rt_multi_render_device_frames call into two device frame buffers on two caller streams
+    (band slots reused every RT_MULTI_SLOTS frames while earlier sends may be in flight).
+    Each buffer ends as the frame of the last camera written to it, bitwise; a frame read
+    on its stream right after its call is complete (caller-stream ordering)."""
+    import torch
+    dev = torch.device("cuda", 0)
+    cfg = scenes.CONFIGS["c2"]
+    prims = scenes.to_prims(cfg.scene())
+    rend.set_scene(prims)
+    W, H = 480, 270
+    cams = [_cam(W, H, 0.05 * k) for k in range(5)]
+    refs = [rend.render(c, 4, capi.RT_PREC_PATH64, 0, capi.RT_OUT_RGB_F32)[0] for c in cams]
+    bufs = [torch.full((H, W, 3), -1.0, dtype=torch.float32, device=dev) for _ in range(2)]
+    sts = [torch.cuda.Stream(dev) for _ in range(2)]
+    torch.cuda.synchronize()
+    with capi.MultiRenderer([0] * n, transport=transport) as m:
+        m.set_scene(prims)
+        nf = 13
+        m.render_device_frames(cams, 4, [b.data_ptr() for b in bufs], capi.RT_PREC_PATH64,
+                               streams=[s.cuda_stream for s in sts], nframes=nf)
+        torch.cuda.synchronize()
+        m.sync()
+        for b in range(2):
+            last = max(f for f in range(nf) if f % 2 == b)
+            got = bufs[b].cpu().numpy()
+            assert np.array_equal(got.view(np.uint32), refs[last % len(cams)].view(np.uint32)), b
+        # per-frame calls: a copy enqueued on the caller's stream right after the call sees
+        # the whole frame (no host synchronisation in between)
+        snaps = []
+        for k in range(6):
+            s = sts[k % 2]
+            m.render_device(cams[k % len(cams)], 4, bufs[k % 2].data_ptr(), capi.RT_PREC_PATH64,
+                            stream=s.cuda_stream)
+            with torch.cuda.stream(s):
+                snaps.append(bufs[k % 2].clone())
+        torch.cuda.synchronize()
+        m.sync()
+        for k, snap in enumerate(snaps):
+            assert np.array_equal(snap.cpu().numpy().view(np.uint32),
+                                  refs[k % len(cams)].view(np.uint32)), k
+
+
+def test_options_and_scene_reach_every_rank(rend):
+    """rt_multi_set_option / rt_multi_set_scene apply to every rank's ctx: a scene swap and
+    options that change only scheduling/culling (output-invariant) keep the frame bitwise
+    the one-GPU frame of the new scene."""
+    sa = scenes.to_prims(scenes.synthetic_scene(8, 4))
+    sb = scenes.to_prims(scenes.synthetic_scene(64, 6))
+    cam = _cam(320, 180)
+    with capi.MultiRenderer([0] * 3, transport=capi.RT_TRANSPORT_COPY) as m:
+        m.set_scene(sa)
+        a, _ = m.render(cam, 4, capi.RT_PREC_PATH64)
+        m.set_scene(sb)
+        m.set_option(capi.RT_OPT_TILE_BINS, 0)
+        m.set_option(capi.RT_OPT_ROW_FEEDBACK, 1)
+        b1, _ = m.render(cam, 6, capi.RT_PREC_PATH64)
+        b2, _ = m.render(cam, 6, capi.RT_PREC_PATH64)
+        with pytest.raises(capi.RTError):
+            m.set_option(999, 1)
+    rend.set_scene(sa)
+    ra, _ = rend.render(cam, 4, capi.RT_PREC_PATH64)
+    rend.set_scene(sb)
+    rb, _ = rend.render(cam, 6, capi.RT_PREC_PATH64)
+    assert np.array_equal(a.view(np.uint32), ra.view(np.uint32))
+    assert np.array_equal(b1.view(np.uint32), rb.view(np.uint32))
+    assert np.array_equal(b2.view(np.uint32), rb.view(np.uint32))
+
+
+def test_create_errors():
+    """RCCL takes one rank per GPU; a device out of range, bad rank layouts and the COPY
+    transport across processes are rejected with the documented status codes."""
+    import ctypes as C
+    lib = capi.load()
+    h = C.c_void_p()
+
+    def create(devs, nranks, first, uid=None, tr=capi.RT_TRANSPORT_RCCL):
+        arr = (C.c_int32 * len(devs))(*devs)
+        st = lib.rt_multi_create(arr, len(devs), nranks, first, uid, tr, C.byref(h))
+        if st == capi.RT_OK:
+            lib.rt_multi_destroy(h)
+        return st
+
+    assert create([0, 0], 2, 0) == capi.RT_ERR_UNSUPPORTED
+    assert create([999], 1, 0) == capi.RT_ERR_NO_DEVICE
+    assert create([0], 2, 1, None) == capi.RT_ERR_INVALID_ARG          # needs the shared id
+    uid = (C.c_uint8 * capi.RT_MULTI_ID_BYTES)()
+    assert create([0], 2, 1, uid, capi.RT_TRANSPORT_COPY) == capi.RT_ERR_UNSUPPORTED
+    assert create([0], 1, 1) == capi.RT_ERR_INVALID_ARG                # rank past nranks
+    assert len(capi.multi_unique_id()) == capi.RT_MULTI_ID_BYTES
