@@ -145,6 +145,8 @@ def main() -> int:
     ap.add_argument("--tiler", default="native", choices=["native", "torch"],
                     help="tiled mode: the C-ABI's rt_multi (RCCL send/recv in C++), or "
                          "rtamd.tiling over torch.distributed")
+    ap.add_argument("--transport", default="rccl", choices=["rccl", "copy"],
+                    help="rt_multi transport (copy: one process only, --local-ranks)")
     ap.add_argument("--local-ranks", type=int, default=1,
                     help="rehearsal only (one process): split the frame over this many ranks "
                          "on this one GPU with the peer-copy transport; not a measurement")
@@ -255,7 +257,7 @@ def main() -> int:
             uid = [capi.multi_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(uid, src=0)
             multi = capi.MultiRenderer([local], nranks=world, first_rank=rank, unique_id=uid[0])
-        elif args.local_ranks > 1:
+        elif args.local_ranks > 1 or args.transport == "copy":
             multi = capi.MultiRenderer([local] * args.local_ranks,
                                        transport=capi.RT_TRANSPORT_COPY)
         else:

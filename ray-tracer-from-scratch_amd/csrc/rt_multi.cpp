@@ -28,7 +28,9 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -118,13 +120,36 @@ int ctx_err(rt_multi* m, const Rank* k, int st, const char* what) {
     return st;
 }
 
+/* RT_MULTI_TRACE=1 (diagnostics): report to stderr every runtime call of the frame path
+ * that holds the host for more than 100 us (a call that waits for the GPU). */
+bool trace_on() {
+    static const bool on = [] {
+        const char* e = std::getenv("RT_MULTI_TRACE");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+struct SlowCall {
+    const char* what;
+    std::chrono::steady_clock::time_point t0;
+    explicit SlowCall(const char* w) : what(w), t0(trace_on() ? std::chrono::steady_clock::now()
+                                                                : std::chrono::steady_clock::time_point{}) {}
+    ~SlowCall() {
+        if (!trace_on()) return;
+        const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+        if (us > 100) std::fprintf(stderr, "rt_multi slow call %.0f us: %s\n", us, what);
+    }
+};
+
 #define MHIP(m, call)                                          \
     do {                                                       \
+        SlowCall sc_(#call);                                   \
         hipError_t e_ = (call);                                \
         if (e_ != hipSuccess) return hip_err((m), e_, #call);  \
     } while (0)
 #define MNCCL(m, call)                                           \
     do {                                                         \
+        SlowCall sc_(#call);                                     \
         ncclResult_t e_ = (call);                                \
         if (e_ != ncclSuccess) return nccl_err((m), e_, #call);  \
     } while (0)
@@ -161,6 +186,7 @@ int enqueue_rank(rt_multi* m, Rank* k, const Job& j) {
     if (k->rank == 0) {
         // the root's band, in place, on the caller's stream
         if (nrows > 0) {
+            SlowCall sc_("rt_render_device (root)");
             st = rt_render_device(k->ctx, &cam, row0, nrows, j.depth, j.precision, j.flags,
                                   j.out_format, j.d_frame + (size_t)row0 * row_bytes, nullptr,
                                   j.stream);
@@ -191,8 +217,11 @@ int enqueue_rank(rt_multi* m, Rank* k, const Job& j) {
     if (st != RT_OK) return st;
     // band buffer `s` is free once the send of frame k - RT_MULTI_SLOTS has completed
     MHIP(m, hipStreamWaitEvent(k->render_stream, k->ev_sent[s], 0));
-    st = rt_render_device(k->ctx, &cam, row0, nrows, j.depth, j.precision, j.flags, j.out_format,
-                          k->band[s], nullptr, k->render_stream);
+    {
+        SlowCall sc_("rt_render_device (band)");
+        st = rt_render_device(k->ctx, &cam, row0, nrows, j.depth, j.precision, j.flags, j.out_format,
+                              k->band[s], nullptr, k->render_stream);
+    }
     if (st != RT_OK) return ctx_err(m, k, st, "rt_render_device");
     MHIP(m, hipEventRecord(k->ev_rendered[s], k->render_stream));
     MHIP(m, hipStreamWaitEvent(k->comm_stream, k->ev_rendered[s], 0));
@@ -286,7 +315,9 @@ int render_frame(rt_multi* m, const rt_camera* cam, int32_t depth, int32_t preci
         MHIP(m, dg.err);
         j.stream = stream ? static_cast<hipStream_t>(stream) : root->render_stream;
         j.ev_in = m->ev_in[slot];
-        MHIP(m, hipEventRecord(j.ev_in, j.stream));
+        // one rank: the band is the frame, rendered in place in stream order; nothing else
+        // writes the frame buffer, so no event is needed (it costs host time every frame)
+        if (m->nranks > 1) MHIP(m, hipEventRecord(j.ev_in, j.stream));
     } else {
         j.stream = static_cast<hipStream_t>(stream);
     }
@@ -302,10 +333,13 @@ int render_frame(rt_multi* m, const rt_camera* cam, int32_t depth, int32_t preci
         k->cv.notify_one();
     }
     int st = enqueue_rank(m, m->r[0], j);
-    for (int L = 1; L < m->nlocal; L++) {
-        Rank* k = m->r[L];
-        while (k->finished.load(std::memory_order_acquire) != m->frame + 1) std::this_thread::yield();
-        if (st == RT_OK && k->status != RT_OK) st = k->status;
+    {
+        SlowCall sc_("waiting for the worker threads");
+        for (int L = 1; L < m->nlocal; L++) {
+            Rank* k = m->r[L];
+            while (k->finished.load(std::memory_order_acquire) != m->frame + 1) std::this_thread::yield();
+            if (st == RT_OK && k->status != RT_OK) st = k->status;
+        }
     }
     m->frame++;
     if (st != RT_OK) return st;

@@ -1,0 +1,91 @@
+#!/usr/bin/env python3
+"""Host cost per frame (µs) of the frame operators, with the GPU held busy behind a spin
+kernel so the host never waits for it: rt_render_device of the whole c2 frame and of a
+1/N band (the per-rank host work of config 4: pixel boxes, row order, launch), a bare
+hipEventRecord, and rt_multi_render_device_frames for one rank (RCCL) and for N ranks on
+this one GPU (peer-copy transport, worker threads)."""
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "ray-tracer-from-scratch_amd"))
+from rtamd import capi, scenes  # noqa: E402
+
+
+def main():
+    import torch
+    dev = torch.device("cuda", 0)
+    sts = [torch.cuda.Stream(dev) for _ in range(2)]
+    cfg = scenes.CONFIGS[os.environ.get("CFG", "c2")]
+    prims = scenes.to_prims(cfg.scene())
+    cam = capi.camera_init(**scenes.camera_args(cfg.width, cfg.height))
+    H, W = cam.height, cam.width
+    outs = [torch.empty((H, W, 3), device=dev) for _ in range(2)]
+    n = int(os.environ.get("N", "100"))
+
+    def timed(fn, nrep=4):
+        best = 1e9
+        for _ in range(nrep):
+            torch.cuda.synchronize()
+            for s in sts:
+                with torch.cuda.stream(s):
+                    torch.cuda._sleep(int(4e8))  # GPU spin ahead of the calls
+            t0 = time.perf_counter()
+            fn()
+            best = min(best, (time.perf_counter() - t0) / n * 1e6)
+            torch.cuda.synchronize()
+        return round(best, 2)
+
+    res = {"cfg": cfg.name, "frames_per_call": n}
+    r = capi.Renderer(0)
+    r.set_scene(prims)
+    r.set_option(capi.RT_OPT_BOX_CACHE, 0)
+    ptrs = [o.data_ptr() for o in outs]
+    sp = [s.cuda_stream for s in sts]
+    res["render_device_full"] = timed(lambda: r.render_device_frames(
+        [cam], cfg.depth, ptrs, capi.RT_PREC_PATH64, streams=sp, nframes=n))
+    for nb in (2, 4, 8):
+        r0, nr = capi.band_rows(H, nb, nb // 2)
+        res[f"render_device_band_1_{nb}"] = timed(lambda: r.render_device_frames(
+            [cam], cfg.depth, ptrs, capi.RT_PREC_PATH64, row0=r0, nrows=nr, streams=sp, nframes=n))
+    ev = torch.cuda.Event()
+
+    def rec():
+        for k in range(n):
+            ev.record(sts[k % 2])
+    res["hipEventRecord"] = timed(rec)
+    # raw HIP copies of a 1/4 frame band (same device), enqueued behind the spin
+    hip = C.CDLL("libamdhip64.so")
+    nbytes = (H // 4) * W * 12
+    src, dst = outs[0].data_ptr(), outs[1].data_ptr()
+    s0 = C.c_void_p(sts[0].cuda_stream)
+    hip.hipMemcpyPeerAsync.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_size_t, C.c_void_p]
+    hip.hipMemcpyAsync.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p]
+    res["hipMemcpyPeerAsync_same_dev"] = timed(lambda: [hip.hipMemcpyPeerAsync(
+        C.c_void_p(dst), 0, C.c_void_p(src), 0, nbytes, s0) for _ in range(n)])
+    res["hipMemcpyAsync_d2d"] = timed(lambda: [hip.hipMemcpyAsync(
+        C.c_void_p(dst), C.c_void_p(src), nbytes, 3, s0) for _ in range(n)])
+    res["hipMemcpyAsync_default"] = timed(lambda: [hip.hipMemcpyAsync(
+        C.c_void_p(dst), C.c_void_p(src), nbytes, 4, s0) for _ in range(n)])
+    r.close()
+    for devs, tr in (([0], capi.RT_TRANSPORT_RCCL), ([0], capi.RT_TRANSPORT_COPY), ([0, 0], capi.RT_TRANSPORT_COPY),
+                     ([0] * 4, capi.RT_TRANSPORT_COPY), ([0] * 8, capi.RT_TRANSPORT_COPY)):
+        with capi.MultiRenderer(devs, transport=tr) as m:
+            m.set_scene(prims)
+            m.set_option(capi.RT_OPT_BOX_CACHE, 0)
+            m.render_device_frames([cam], cfg.depth, ptrs, capi.RT_PREC_PATH64, streams=sp,
+                                   nframes=4)
+            torch.cuda.synchronize()
+            res[f"multi_{len(devs)}_{'rccl' if tr == 0 else 'copy'}"] = timed(
+                lambda: m.render_device_frames([cam], cfg.depth, ptrs, capi.RT_PREC_PATH64,
+                                               streams=sp, nframes=n))
+            torch.cuda.synchronize()
+            m.sync()
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
