@@ -14,7 +14,8 @@ import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_DIR = os.path.join(PKG_DIR, "lib")
-LIB_PATH = os.path.join(LIB_DIR, "librt_amd.so")
+# RT_AMD_LIB: another build of the same C-ABI (the host sanitizer build of `make asan`)
+LIB_PATH = os.environ.get("RT_AMD_LIB") or os.path.join(LIB_DIR, "librt_amd.so")
 HOST_LIB_PATH = os.path.join(LIB_DIR, "librt_host.so")
 
 # ---- enums (rt_capi.h) ----------------------------------------------------

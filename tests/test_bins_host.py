@@ -126,3 +126,64 @@ def test_frame_boxes_errors():
     # too many primitives for the linear-scan bins: no boxes
     b, m, d = capi.frame_boxes(scenes.to_prims(scenes.synthetic_scene(70, 0)), cam)
     assert len(b) == 0 and d == 0
+
+
+def test_frame_boxes_fuzz_bounds_and_capacity():
+    """Host-code fuzz of the per-frame box assembly (rt_capi.cpp pack_scene, frame_boxes,
+    boxes_for, the mirror-chain levels) — the hand-indexed host code `tools/asan_check.sh`
+    runs under AddressSanitizer/UBSan: random scene sizes up to past the 64-primitive bin
+    limit and 20 walls (mirror levels shrink with nW), degenerate primitives (zero and
+    negative radii, z-normal and NaN-normal walls, far coordinates), cameras inside
+    primitives and with extreme fields of view, random row bands, and capacities exactly
+    at and one below the box count.  Every returned box lies in the frame/band widened by
+    one pixel (or is the empty marker)."""
+    rng = np.random.default_rng(2024)
+    for trial in range(120):
+        ns, nw = int(rng.integers(0, 70)), int(rng.integers(0, 21))
+        sc = scenes.synthetic_scene(min(ns, 60), min(nw, 6), seed=int(rng.integers(1 << 30)))
+        for _ in range(max(0, nw - 6)):
+            nrm = rng.normal(size=3)
+            if rng.random() < 0.15:
+                nrm = np.array([0.0, 0.0, 1.0])           # never hit (NaN basis)
+            sc.append(scenes.Wall(scenes.Material((.5, .5, .5), .5),
+                                  tuple(rng.uniform(-30, 30, 3)), tuple(nrm / np.linalg.norm(nrm)),
+                                  float(rng.uniform(0, 9)), float(rng.uniform(0, 9))))
+        for _ in range(max(0, ns - 60)):
+            sc.append(scenes.Sphere(scenes.Material((.3, .3, .3), .2),
+                                    tuple(rng.uniform(-1e3, 1e3, 3)), float(rng.uniform(-1, 3))))
+        if sc and rng.random() < 0.2:
+            sc[0] = scenes.Sphere(scenes.Material((1, 1, 1), .5), (0.0, 0.0, 0.0), 0.0)
+        prims = scenes.to_prims(sc)
+        pos = rng.uniform([-2, -4, -2], [9, 4, 2])
+        look = pos + rng.normal(size=3)
+        vfov = float(rng.choice([0.5, 30.0, 90.0, 170.0, 179.9]))
+        w = int(rng.choice([1, 8, 63, 200]))
+        cam = capi.camera_init(pos, look, (0, 0, -1), vfov, float(rng.choice([1.0, 16 / 9, 0.3])), float(w))
+        if cam.height <= 0:
+            continue
+        r0 = int(rng.integers(0, cam.height))
+        nr = int(rng.integers(0, cam.height - r0 + 1))
+        lib = capi.load()
+        arr = (capi.rt_prim * max(1, len(prims)))(*prims)
+        nb, md = capi.C.c_int32(), capi.C.c_int32()
+        st = lib.rt_frame_boxes(arr, len(prims), capi.C.byref(cam), r0, nr, None, 0,
+                                capi.C.byref(nb), capi.C.byref(md))
+        # walls that can be hit (z-normal ones are not uploaded): nbox = spheres + those
+        n_w = nb.value - sum(1 for o in sc if o.kind == capi.RT_PRIM_SPHERE) if nb.value else 0
+        total = nb.value * sum(n_w ** L for L in range(md.value + 1))
+        assert st == (capi.RT_OK if total == 0 else capi.RT_ERR_INVALID_ARG), trial
+        if total == 0:
+            continue
+        out = np.full((total + 1, 4), 12345, np.int16)
+        ptr = out.ctypes.data_as(capi.C.POINTER(capi.C.c_int16))
+        if total > 1:   # one box short of the count: rejected, nothing written past cap
+            assert lib.rt_frame_boxes(arr, len(prims), capi.C.byref(cam), r0, nr, ptr, total - 1,
+                                      capi.C.byref(nb), capi.C.byref(md)) == capi.RT_ERR_INVALID_ARG
+        assert lib.rt_frame_boxes(arr, len(prims), capi.C.byref(cam), r0, nr, ptr, total,
+                                  capi.C.byref(nb), capi.C.byref(md)) == capi.RT_OK
+        assert (out[total] == 12345).all()
+        b = out[:total]
+        empty = (b[:, 0] > b[:, 1]) | (b[:, 2] > b[:, 3])
+        ok = empty | ((b[:, 0] >= -1) & (b[:, 1] <= cam.width) & (b[:, 2] >= r0 - 1) &
+                      (b[:, 3] <= r0 + nr))
+        assert ok.all(), trial
