@@ -1,0 +1,86 @@
+#!/usr/bin/env python3
+"""Inputs of the row-tiled scaling model, measured on ONE MI355X: for each
+split N in {1, 2, 4, 8} of a config's frame into rt_band_rows bands, every band's
+one-stream kernel time (its own ctx, measured row order warm, HIP events around
+back-to-back launches), its host time per frame (rt_render_device with the GPU held busy),
+and the bytes it sends to the root.  The gather term needs the xGMI link rate, which one
+GPU cannot measure: the model takes it as a parameter.
+    python tools/band_model.py [--config c2] [--precision path64]"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "ray-tracer-from-scratch_amd"))
+from rtamd import capi, scenes  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--precision", default="path64")
+    ap.add_argument("--launches", type=int, default=100)
+    args = ap.parse_args()
+    import torch
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.Stream(dev)
+    cfg = scenes.CONFIGS[args.config]
+    prims = scenes.to_prims(cfg.scene())
+    cam = capi.camera_init(**scenes.camera_args(cfg.width, cfg.height))
+    H, W = cam.height, cam.width
+    prec = capi.PRECISIONS[args.precision]
+    out = torch.empty((H, W, 3), device=dev)
+    segs = torch.zeros(1, dtype=torch.int64, device=dev)
+    n = args.launches
+    res = {"config": args.config, "precision": args.precision, "width": W, "height": H,
+           "splits": {}}
+    for N in (1, 2, 4, 8):
+        bands = []
+        for r in range(N):
+            r0, nr = capi.band_rows(H, N, r)
+            rend = capi.Renderer(0)
+            rend.set_scene(prims)
+            for _ in range(40):   # warm: the measured row order for this band settles
+                rend.render_device(cam, cfg.depth, out.data_ptr(), prec, row0=r0, nrows=nr,
+                                   stream=st.cuda_stream)
+            segs.zero_()
+            rend.render_device(cam, cfg.depth, out.data_ptr(), prec, row0=r0, nrows=nr,
+                               d_segments=segs.data_ptr(), stream=st.cuda_stream)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            rend.render_device_frames([cam], cfg.depth, [out.data_ptr()], prec, row0=r0, nrows=nr,
+                                      streams=[st.cuda_stream], nframes=n)
+            e1.record(st)
+            torch.cuda.synchronize()
+            kms = e0.elapsed_time(e1) / n
+            # host time per frame: launches queued behind a GPU spin, so the host never waits
+            with torch.cuda.stream(st):
+                torch.cuda._sleep(int(2e8))
+            t0 = time.perf_counter()
+            rend.render_device_frames([cam], cfg.depth, [out.data_ptr()], prec, row0=r0, nrows=nr,
+                                      streams=[st.cuda_stream], nframes=n)
+            host_us = (time.perf_counter() - t0) / n * 1e6
+            torch.cuda.synchronize()
+            rend.close()
+            bands.append({"rank": r, "row0": r0, "nrows": nr, "kernel_us": round(kms * 1e3, 2),
+                          "host_us": round(host_us, 2), "segments": int(segs.item()),
+                          "send_bytes_f32": 0 if r == 0 else nr * W * 12,
+                          "send_bytes_rgba8": 0 if r == 0 else nr * W * 4})
+        res["splits"][N] = {
+            "bands": bands,
+            "max_kernel_us": max(b["kernel_us"] for b in bands),
+            "max_host_us": max(b["host_us"] for b in bands),
+            "root_in_bytes_f32": sum(b["send_bytes_f32"] for b in bands),
+            "root_in_bytes_rgba8": sum(b["send_bytes_rgba8"] for b in bands),
+            "max_link_bytes_f32": max(b["send_bytes_f32"] for b in bands),
+        }
+        print(json.dumps({"N": N, **{k: v for k, v in res["splits"][N].items() if k != "bands"}}),
+              file=sys.stderr, flush=True)
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
