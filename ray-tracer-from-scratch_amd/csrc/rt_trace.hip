@@ -153,8 +153,14 @@ __device__ unsigned long long g_diag[16];
 #ifndef RT_WPE_F32_BONUS
 #define RT_WPE_F32_BONUS 0
 #endif
+#ifndef RT_WPE_CULL64_BONUS  // F64/MIXED cull kernels: one wave/SIMD more since the recursion
+#define RT_WPE_CULL64_BONUS 1    // stack moved to LDS (A/B: c5 F64 -3.5%, c3 F64 -5.6% vs 4 waves)
+#endif
 #ifndef RT_WPE_F64_LIN_BONUS
 #define RT_WPE_F64_LIN_BONUS 0
+#endif
+#ifndef RT_STACK_LDS      // 1: the cull kernels keep the recursion stack in LDS (trace_pixel_d)
+#define RT_STACK_LDS 1
 #endif
 #ifndef RT_F32_READLANE   // F32 survivor records: 1 = v_readlane from the culling lane,
 #define RT_F32_READLANE 0 // 0 = scalar loads (A/B: c5 -13%); fp64 paths keep v_readlane
@@ -691,6 +697,20 @@ __device__ __forceinline__ RayF make_rayf(const RayD& r) {
     rf.oinf = fmax3abs(rf.o.x, rf.o.y, rf.o.z);
     return rf;
 }
+/* DBL_MAX as an opaque scalar (SGPR pair): as a literal the register allocator of the deep
+ * cull kernels kept it in a VGPR pair and spilled that to scratch, reloading it inside the
+ * sphere loop; from SGPRs each use is a plain copy.  (The linear-scan kernels, which did not
+ * spill, keep the literal: A/B c1 +2..12% otherwise.) */
+#ifndef RT_DMAX_SGPR
+#define RT_DMAX_SGPR 1
+#endif
+__device__ __forceinline__ double dbl_max_s() {
+    if (!RT_DMAX_SGPR) return DBL_MAX;
+    uint32_t lo, hi;
+    asm("s_mov_b32 %0, -1" : "=s"(lo));
+    asm("s_mov_b32 %0, 0x7fefffff" : "=s"(hi));
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
 __device__ __forceinline__ HitD no_hit() {
     HitD h;
     h.dist = DBL_MAX;
@@ -1117,6 +1137,7 @@ template <bool MIXED, bool CULL, bool CLU>
 __device__ __forceinline__ HitD scan_d(const KParams& p, const RayD& r, bool alive,
                                        bool primary, bool binned, uint64_t keep) {
     HitD h = no_hit();
+    if (CULL) h.dist = dbl_max_s();  // the deep kernels (see dbl_max_s)
     if (CULL) {
         // walls first: their distances then bound the sphere tests
         RayF rf;
@@ -1210,9 +1231,40 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
     }
     const uint64_t smask = p.nS >= 64 ? ~0ull : (1ull << p.nS) - 1;
 
-    CT st_s[MAXD];
-    CT st_k[MAXD];
-    int st_m[MAXD];
+    // The register stack of the recursion (per level: shading scalar, sun scalar, material
+    // slot).  In the cull kernels (deep configs) it lives in LDS instead (RT_STACK_LDS): a
+    // VGPR array indexed by the runtime bounce counter costs a select per element on every
+    // push and holds 2-3 VGPRs per level for the whole bounce loop, which is what the deep
+    // fp64 kernels spilled to scratch.  LDS: one ds_write per value per bounce, one read
+    // per level in the unwind, [level][lane] so a wave's accesses are conflict-free.
+    constexpr bool LSTK = RT_STACK_LDS && CULL;
+    __shared__ CT lds_s[LSTK ? MAXD * BLOCK : 1];
+    __shared__ CT lds_k[(LSTK && SUN) ? MAXD * BLOCK : 1];
+    __shared__ int lds_m[LSTK ? MAXD * BLOCK : 1];
+    CT st_s[LSTK ? 1 : MAXD];
+    CT st_k[LSTK ? 1 : MAXD];
+    int st_m[LSTK ? 1 : MAXD];
+    const int tid = (int)threadIdx.x;
+    auto push = [&](int k, CT sv, CT kv, int mv) __attribute__((always_inline)) {
+        if constexpr (LSTK) {
+            lds_s[k * BLOCK + tid] = sv;
+            if (SUN) lds_k[k * BLOCK + tid] = kv;
+            lds_m[k * BLOCK + tid] = mv;
+        } else {
+            st_s[k] = sv;
+            st_k[k] = kv;
+            st_m[k] = mv;
+        }
+    };
+    auto ld_s = [&](int q) __attribute__((always_inline)) -> CT {
+        if constexpr (LSTK) return lds_s[q * BLOCK + tid]; else return st_s[q];
+    };
+    auto ld_k = [&](int q) __attribute__((always_inline)) -> CT {
+        if constexpr (LSTK) return SUN ? lds_k[q * BLOCK + tid] : (CT)0; else return st_k[q];
+    };
+    auto ld_m = [&](int q) __attribute__((always_inline)) -> int {
+        if constexpr (LSTK) return lds_m[q * BLOCK + tid]; else return st_m[q];
+    };
     int n = 0;
     d3 c64 = D3(0, 0, 0);
     f3 c32 = F3(0.f, 0.f, 0.f);
@@ -1314,9 +1366,7 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
             alive = false;
             return;
         }
-        st_s[k] = s;
-        st_k[k] = ks;
-        st_m[k] = h.slot;
+        push(k, s, ks, h.slot);
         n = k + 1;
         // start + reflect(d, N) (main.cpp:111-113, vec.cpp:51-57)
         const double cc = 2 * dot(nv, nn);
@@ -1370,13 +1420,14 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
     STAGE(3);
     for (int q = MAXD - 1; q >= 0; --q) {
         if ((!RT_UNWIND_KEND || q < kend) && q < n) {  // uniform test: levels no lane reached
-            const DevMat& m = p.mat[st_m[q]];
+            const int mq = ld_m(q);
+            const DevMat& m = p.mat[mq];
             if (COLOR64) {
-                const d3 L = local_color_d(m, st_s[q], st_k[q], sun);
+                const d3 L = local_color_d(m, ld_s(q), ld_k(q), sun);
                 c64 = lerp(L, c64, m.km);  // vec.cpp:45-49 via main.cpp:117
             } else {
-                const DevMat32& m32 = p.mat32[st_m[q]];
-                const f3 L = local_color_f(m32, st_s[q], st_k[q], sun);
+                const DevMat32& m32 = p.mat32[mq];
+                const f3 L = local_color_f(m32, ld_s(q), ld_k(q), sun);
                 const float km = m32.km;
                 c32 = F3(fmaf(km, c32.x - L.x, L.x), fmaf(km, c32.y - L.y, L.y),
                          fmaf(km, c32.z - L.z, L.z));
@@ -2085,8 +2136,21 @@ constexpr int waves_per_eu() {
             ((!CULL && !SUN && tier == 0) ? RT_WPE_PATH64_LIN_BONUS : 0);
     else
         w = (INT_EXP ? (SUN ? 3 : 4) : (SUN ? 2 : 3)) - (tier > 0 ? 1 : 0) -
-            ((PREC == PREC_MIXED && CULL && MAXD >= 8) ? RT_WPE_MIXED_CULL_DROP : 0);
+            ((PREC == PREC_MIXED && CULL && MAXD >= 8) ? RT_WPE_MIXED_CULL_DROP : 0) +
+            (CULL ? RT_WPE_CULL64_BONUS : 0);
     return w < 2 ? 2 : w;
+}
+
+/* The store's pixel coordinates are formed again after the trace from the wave-uniform
+ * tile (SGPRs) and the lane id read with v_mbcnt (not threadIdx.x, so the compiler cannot
+ * merge it with the first computation): otherwise x, r and the valid flag stay live across
+ * the whole bounce loop, and in the deep cull kernels (c5) they were what the register
+ * allocator spilled to scratch — one store and one reload per lane, 12 B each. */
+#ifndef RT_STORE_RECOMPUTE
+#define RT_STORE_RECOMPUTE 1
+#endif
+__device__ __forceinline__ int lane_mbcnt() {
+    return (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
 }
 
 /* One tile per wave: tile column bx, tile row trow (after the row order), gx tile columns. */
@@ -2105,9 +2169,19 @@ __device__ __forceinline__ void trace_tile(const KParams& p, int bx, int trow, i
     const int i = p.row0 + r;
     int segs = 0;
     // every lane runs the (converged) bounce loop; only valid lanes trace and store
+    // the store's coordinates (see RT_STORE_RECOMPUTE)
+    auto store = [&](double cr, double cg, double cb) __attribute__((always_inline)) {
+        if (RT_STORE_RECOMPUTE && CULL && BLOCK == 64) {  // (linear kernels: no spill, A/B +1..12%)
+            const int l2 = lane_mbcnt();
+            const int xs = bx * TILE_W + (l2 & 7), rs = trow * TILE_H + (l2 >> 3);
+            if (xs < p.W && rs < p.nrows) store_pixel(p, rs, xs, cr, cg, cb);
+        } else if (valid) {
+            store_pixel(p, r, x, cr, cg, cb);
+        }
+    };
     if (PREC == PREC_F32) {
         const f3 c = trace_pixel_f<SUN, CULL, MAXD>(p, x, i, valid, segs, t_tile, braw);
-        if (valid) store_pixel(p, r, x, c.x, c.y, c.z);
+        store(c.x, c.y, c.z);
     } else {
 #if RT_STAGE_TIMES
         uint64_t g_stage[8];
@@ -2120,7 +2194,7 @@ __device__ __forceinline__ void trace_tile(const KParams& p, int bx, int trow, i
             trace_pixel_d<PREC == PREC_MIXED, PREC != PREC_PATH64, SUN, INT_EXP, CULL, MAXD>(
                 p, x, i, valid, segs, t_tile, braw);
 #endif
-        if (valid) store_pixel(p, r, x, c.x, c.y, c.z);
+        store(c.x, c.y, c.z);
 #if RT_STAGE_TIMES
         STAGE(5);
         {
