@@ -15,10 +15,11 @@
  *     the caller's stream; RCCL: the comm stream waits for the caller's earlier work (the
  *     buffer may still be read), receives every other band into its rows (one
  *     ncclGroupStart/End), and the caller's stream waits for it.
- *   other ranks: the render stream waits until band buffer `slot` has been sent (frame
+ *   other ranks: slot s's render stream waits until band buffer s has been sent (frame
  *     k - RT_MULTI_SLOTS), renders the band into it, and the comm stream sends it once the
  *     render is done (RCCL ncclSend, or a peer copy into the root's rows for
- *     RT_TRANSPORT_COPY) — so the render of frame k+1 overlaps the send of frame k.
+ *     RT_TRANSPORT_COPY) — so the render of frame k+1 overlaps the send of frame k, and the
+ *     tail of frame k's band kernel (one slot's stream) overlaps frame k+1's (the other's).
  * One process driving several GPUs runs the extra ranks' host work (pixel boxes, row order,
  * launch: rt_render_device) on one worker thread per rank, in parallel with the caller's
  * thread, which does the root's.
@@ -59,7 +60,11 @@ struct Rank {
     int device = 0;
     rt_ctx* ctx = nullptr;
     ncclComm_t comm = nullptr;
-    hipStream_t render_stream = nullptr, comm_stream = nullptr;
+    // one render stream per band slot: consecutive frames' band kernels overlap, so a rank's
+    // frame rate is not bounded by its heaviest wave's latency (a c2 band's kernel takes
+    // ~20 us for 1/8 of the frame: the tail, tools/band_model.py)
+    hipStream_t render_stream[RT_MULTI_SLOTS] = {nullptr, nullptr};
+    hipStream_t comm_stream = nullptr;
     void* band[RT_MULTI_SLOTS] = {nullptr, nullptr};
     size_t band_cap = 0;
     hipEvent_t ev_rendered[RT_MULTI_SLOTS] = {nullptr, nullptr};
@@ -160,7 +165,7 @@ int bpp(int32_t f) { return rt_out_bytes_per_pixel(f); }
 int ensure_bands(rt_multi* m, Rank* k, size_t bytes) {
     if (bytes <= k->band_cap) return RT_OK;
     // nothing in flight may still read or write the old buffers
-    MHIP(m, hipStreamSynchronize(k->render_stream));
+    for (auto rs : k->render_stream) MHIP(m, hipStreamSynchronize(rs));
     MHIP(m, hipStreamSynchronize(k->comm_stream));
     for (auto& b : k->band) {
         if (b) MHIP(m, hipFree(b));
@@ -216,14 +221,14 @@ int enqueue_rank(rt_multi* m, Rank* k, const Job& j) {
     st = ensure_bands(m, k, (size_t)((cam.height + m->nranks - 1) / m->nranks) * row_bytes);
     if (st != RT_OK) return st;
     // band buffer `s` is free once the send of frame k - RT_MULTI_SLOTS has completed
-    MHIP(m, hipStreamWaitEvent(k->render_stream, k->ev_sent[s], 0));
+    MHIP(m, hipStreamWaitEvent(k->render_stream[s], k->ev_sent[s], 0));
     {
         SlowCall sc_("rt_render_device (band)");
         st = rt_render_device(k->ctx, &cam, row0, nrows, j.depth, j.precision, j.flags, j.out_format,
-                              k->band[s], nullptr, k->render_stream);
+                              k->band[s], nullptr, k->render_stream[s]);
     }
     if (st != RT_OK) return ctx_err(m, k, st, "rt_render_device");
-    MHIP(m, hipEventRecord(k->ev_rendered[s], k->render_stream));
+    MHIP(m, hipEventRecord(k->ev_rendered[s], k->render_stream[s]));
     MHIP(m, hipStreamWaitEvent(k->comm_stream, k->ev_rendered[s], 0));
     if (m->transport == RT_TRANSPORT_RCCL) {
         MNCCL(m, ncclSend(k->band[s], bytes, ncclUint8, 0, k->comm, k->comm_stream));
@@ -270,7 +275,8 @@ void destroy_rank(Rank* k) {
         k->th.join();
     }
     DevGuard dg(k->device);
-    if (k->render_stream) (void)hipStreamSynchronize(k->render_stream);
+    for (auto rs : k->render_stream)
+        if (rs) (void)hipStreamSynchronize(rs);
     if (k->comm_stream) (void)hipStreamSynchronize(k->comm_stream);
     if (k->comm) (void)ncclCommDestroy(k->comm);
     for (auto& b : k->band)
@@ -280,7 +286,8 @@ void destroy_rank(Rank* k) {
         if (k->ev_sent[s]) (void)hipEventDestroy(k->ev_sent[s]);
     }
     if (k->ev_done) (void)hipEventDestroy(k->ev_done);
-    if (k->render_stream) (void)hipStreamDestroy(k->render_stream);
+    for (auto rs : k->render_stream)
+        if (rs) (void)hipStreamDestroy(rs);
     if (k->comm_stream) (void)hipStreamDestroy(k->comm_stream);
     if (k->ctx) (void)rt_ctx_destroy(k->ctx);
     delete k;
@@ -313,7 +320,7 @@ int render_frame(rt_multi* m, const rt_camera* cam, int32_t depth, int32_t preci
         if (!d_frame && (size_t)cam->width * cam->height > 0) return RT_ERR_INVALID_ARG;
         DevGuard dg(root->device);
         MHIP(m, dg.err);
-        j.stream = stream ? static_cast<hipStream_t>(stream) : root->render_stream;
+        j.stream = stream ? static_cast<hipStream_t>(stream) : root->render_stream[slot];
         j.ev_in = m->ev_in[slot];
         // one rank: the band is the frame, rendered in place in stream order; nothing else
         // writes the frame buffer, so no event is needed (it costs host time every frame)
@@ -417,7 +424,8 @@ int rt_multi_create(const int32_t* devices, int32_t nlocal, int32_t nranks, int3
         }
         DevGuard dg(k->device);
         hipError_t e = dg.err;
-        if (e == hipSuccess) e = hipStreamCreateWithFlags(&k->render_stream, hipStreamNonBlocking);
+        for (auto& rs : k->render_stream)
+            if (e == hipSuccess) e = hipStreamCreateWithFlags(&rs, hipStreamNonBlocking);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&k->comm_stream, hipStreamNonBlocking);
         for (int s = 0; s < RT_MULTI_SLOTS && e == hipSuccess; s++) {
             e = hipEventCreateWithFlags(&k->ev_rendered[s], hipEventDisableTiming);
@@ -453,7 +461,9 @@ int rt_multi_create(const int32_t* devices, int32_t nlocal, int32_t nranks, int3
             }
         }
     }
-    if (st == RT_OK && transport == RT_TRANSPORT_RCCL) {
+    // one rank: the band is the frame and nothing is exchanged, so no communicator (RCCL's
+    // init would only print its banner on stdout and start its proxy thread)
+    if (st == RT_OK && transport == RT_TRANSPORT_RCCL && nranks > 1) {
         ncclUniqueId id;
         if (one_process && !unique_id) {
             if (ncclGetUniqueId(&id) != ncclSuccess) fail(nccl_err(m, ncclInternalError, "ncclGetUniqueId"));
@@ -602,7 +612,7 @@ int rt_multi_sync(rt_multi* m) {
     for (Rank* k : m->r) {
         DevGuard dg(k->device);
         MHIP(m, dg.err);
-        MHIP(m, hipStreamSynchronize(k->render_stream));
+        for (auto rs : k->render_stream) MHIP(m, hipStreamSynchronize(rs));
         MHIP(m, hipStreamSynchronize(k->comm_stream));
         if (k->comm) {
             ncclResult_t async = ncclSuccess;
