@@ -20,8 +20,10 @@ Rays = segments = closest-hit queries (primary + reflection), counted exactly by
 kernel in an untimed census launch.
 
 Order of a run: census; side measurements (per-precision kernel sweep, sun-on frame loop,
-moving-camera frame loop — before the timed region, so it starts on a GPU at its running
-clock); W warmup + K timed steps, each enqueued by one C-ABI call per region
+moving-camera frame loop, and `steady_state`: the timed loop itself over 200 frames —
+before the timed region, so it starts on a GPU at its running clock with the measured
+tile-row order settled, as inside a running frame loop); W warmup + K timed steps, each
+enqueued by one C-ABI call per region
 (rt_multi_render_device_frames / rt_render_device_frames: every frame's own host work and
 launch, as a C++ frame loop does them, without Python's per-call overhead); the one-stream
 kernel time; the frame-sharded side run (N > 1); the CPU baseline (rank 0, N = 1).
@@ -375,11 +377,42 @@ def main() -> int:
                     mv_segs / len(cams) / (ms * 1e-3) / 1e6, 1)
             rend.set_option(capi.RT_OPT_ROW_FEEDBACK, args.row_feedback)
 
-    # the side loops left the row feedback holding another view's order: drop it (with any
-    # snapshot still in flight), so the first warmup frame samples this camera afresh, with
-    # frames in flight as the timed steps run them
+    # the side loops left `rend`'s row feedback holding another view's order: drop it (with
+    # any snapshot still in flight), so its next frame samples this camera afresh
     rend.set_option(capi.RT_OPT_ROW_FEEDBACK, 0)
     rend.set_option(capi.RT_OPT_ROW_FEEDBACK, args.row_feedback)
+
+    # ---- steady state: the timed loop itself over 200 frames (a side measurement, before
+    # the warmup).  It also leaves the product path's measured tile-row order settled for
+    # this camera, as in a running frame loop; without it a short timed region (the driver
+    # runs 20 steps) spends its first frames on the order's ramp-up (measured: 20-step
+    # regions 33-40 us/frame vs 29 over 200 frames) ----
+    steady = None
+    if not args.no_sweep:
+        nst = 200
+        torch.cuda.synchronize(dev)
+        if multi is not None:
+            multi.sync()
+        barrier()
+        es0 = torch.cuda.Event(enable_timing=True)
+        es1 = torch.cuda.Event(enable_timing=True)
+        ts0 = time.perf_counter()
+        es0.record(stream)
+        for s_ in streams[1:]:
+            s_.wait_stream(stream)
+        run_steps(nst)
+        join_streams()
+        es1.record(stream)
+        torch.cuda.synchronize(dev)
+        if multi is not None:
+            multi.sync()
+        barrier()
+        tst = torch.tensor([time.perf_counter() - ts0], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(tst, op=dist.ReduceOp.MAX)
+        steady = {"frames": nst, "ms_per_step": round(float(tst.item()) / nst * 1e3, 4),
+                  "mrays_per_s": round(total_segs * nst / float(tst.item()) / 1e6, 1),
+                  "stream_ms_per_step": round(es0.elapsed_time(es1) / nst, 4)}
 
     # ---- warmup + timed region ----
     run_steps(args.warmup)
@@ -409,9 +442,12 @@ def main() -> int:
     stream_ms = ev0.elapsed_time(ev1) / args.steps
 
     # ---- per-launch kernel time: this rank's rows, one stream, launches back to back ----
+    # (after 64 untimed frames of `rend`, whose measured row order the side loops reset)
+    rend.render_device_frames([cam], depth, [out.data_ptr()], prec, flags, out_fmt, row0=row0,
+                              nrows=nrows, streams=[stream.cuda_stream], nframes=64)
     ek0 = torch.cuda.Event(enable_timing=True)
     ek1 = torch.cuda.Event(enable_timing=True)
-    nk = max(10, args.steps)
+    nk = max(50, args.steps)
     ek0.record(stream)
     rend.render_device_frames([cam], depth, [out.data_ptr()], prec, flags, out_fmt, row0=row0,
                               nrows=nrows, streams=[stream.cuda_stream], nframes=nk)
@@ -542,6 +578,7 @@ def main() -> int:
             "precision_sweep": sweep or None,
             "sun_extension": sun_ext,
             "moving_camera": moving,
+            "steady_state": steady,
             "frame_sharded": sharded,
         }
         if world == 1 and not args.no_cpu_baseline and args.cpu_seconds > 0:
