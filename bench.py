@@ -458,17 +458,18 @@ def main() -> int:
     # ---- N > 1 side run: the weak (frame-sharded) layout, same frame loop, no collective --
     sharded = None
     if tiled_mode and world > 1 and not args.no_sweep:
-        segs_t.zero_()
-        rend.render_device(cam_fly, depth, out.data_ptr(), prec, flags, capi.RT_OUT_RGB_F32,
-                           d_segments=segs_t.data_ptr(), stream=stream.cuda_stream)
-        torch.cuda.synchronize(dev)
-        t_segs = segs_t.clone()
-        dist.all_reduce(t_segs, op=dist.ReduceOp.SUM)
+        # whole frames on every rank: full-size buffers (a non-root rank's `outs` hold a band)
         if full:
             fl_outs = out_ptrs
         else:
             fl_bufs = [torch.empty((H, W, 3), dtype=torch.float32, device=dev) for _ in range(fif)]
             fl_outs = [b.data_ptr() for b in fl_bufs]
+        segs_t.zero_()
+        rend.render_device(cam_fly, depth, fl_outs[0], prec, flags, capi.RT_OUT_RGB_F32,
+                           d_segments=segs_t.data_ptr(), stream=stream.cuda_stream)
+        torch.cuda.synchronize(dev)
+        t_segs = segs_t.clone()
+        dist.all_reduce(t_segs, op=dist.ReduceOp.SUM)
         nfs = max(20, args.steps // 2)
         rend.render_device_frames([cam_fly], depth, fl_outs, prec, flags, out_fmt,
                                   streams=st_ptrs, nframes=args.warmup)
@@ -485,6 +486,30 @@ def main() -> int:
                    "unit": "Mrays/s", "scaling": "weak", "frames_per_step": world,
                    "ms_per_step": round(float(ts.item()) / nfs * 1e3, 4),
                    "parallelism": f"frame-sharded x{world} (fly-through, no collective)"}
+
+    # ---- N > 1 side run: the same row-tiled frames with the RGBA8 epilogue as transport
+    # (4 B/px instead of 12: the root's inbound bytes, which bound config 4, shrink 3x) ----
+    tiled8 = None
+    if multi is not None and world > 1 and args.out == "rgb_f32" and not args.no_sweep:
+        n8 = max(50, args.steps)
+        multi.render_device_frames([cam], depth, out_ptrs if multi.has_root else [], prec, flags,
+                                   capi.RT_OUT_RGBA8, streams=st_ptrs if multi.has_root else st_ptrs[:1],
+                                   nframes=args.warmup)
+        torch.cuda.synchronize(dev)
+        multi.sync()
+        barrier()
+        t80 = time.perf_counter()
+        multi.render_device_frames([cam], depth, out_ptrs if multi.has_root else [], prec, flags,
+                                   capi.RT_OUT_RGBA8, streams=st_ptrs if multi.has_root else st_ptrs[:1],
+                                   nframes=n8)
+        torch.cuda.synchronize(dev)
+        multi.sync()
+        barrier()
+        t8 = torch.tensor([time.perf_counter() - t80], dtype=torch.float64, device=dev)
+        dist.all_reduce(t8, op=dist.ReduceOp.MAX)
+        tiled8 = {"frames": n8, "output": "rgba8 (4 B/px gathered)",
+                  "ms_per_step": round(float(t8.item()) / n8 * 1e3, 4),
+                  "value": round(total_segs * n8 / float(t8.item()) / 1e6, 2), "unit": "Mrays/s"}
 
     result = None
     if rank == 0:
@@ -580,6 +605,7 @@ def main() -> int:
             "moving_camera": moving,
             "steady_state": steady,
             "frame_sharded": sharded,
+            "tiled_rgba8": tiled8,
         }
         if world == 1 and not args.no_cpu_baseline and args.cpu_seconds > 0:
             result["cpu_baseline"] = cpu_baseline(cfg, prims, cam0, depth, flags, args.cpu_seconds)
