@@ -196,6 +196,11 @@ enum rt_option {
                                          best hit skips its bounds test; 0 (default) = scene
                                          order (measured: c2 +1% with the order).  Output is
                                          identical (wall ties compare scene indices). */
+    RT_OPT_MULTI_LAYOUT = 13,         /* rt_multi_set_option only: 0 (default) = contiguous
+                                         row bands (rt_band_rows); 1 = interleaved tile rows
+                                         (rt_interleaved_rows): balanced when the frame's cost
+                                         is concentrated in some rows (config 5).  The
+                                         gathered frame is identical. */
     RT_OPT_CLUSTER_COS = 12           /* C in [-2000, 2000] (default 400): in scenes that use
                                          the wave cull, a RT_PREC_PATH64 or RT_PREC_F32
                                          wave (their cull kernels) whose live
@@ -317,6 +322,21 @@ int rt_multi_render(rt_multi* m, const rt_camera* cam, int32_t depth, int32_t pr
 /* Waits for every frame this process enqueued; RT_ERR_COMM if RCCL reported an
  * asynchronous error. */
 int rt_multi_sync(rt_multi* m);
+
+/* Interleaved parts: the frame's tile rows (8 pixel rows each; the last may be shorter)
+ * dealt round-robin to nparts parts — part p owns tile rows p, p + nparts, p + 2 nparts, ...
+ * — so every part gets a share of the frame's heavy and light rows (rt_multi's balanced
+ * layout, RT_OPT_MULTI_LAYOUT).  *nrows = the part's pixel rows. */
+int rt_interleaved_rows(int32_t height, int32_t nparts, int32_t part, int32_t* nrows);
+
+/* rt_render_device for interleaved part `part` of `nparts`: out_frame_rows == 0 stores the
+ * part's rows back to back in frame order (rt_interleaved_rows x width pixels in d_out);
+ * != 0 stores every row at its frame row (d_out is the whole frame; the other parts' rows
+ * are not touched).  nparts == 1 is the whole frame. */
+int rt_render_device_interleaved(rt_ctx* ctx, const rt_camera* cam, int32_t nparts, int32_t part,
+                                 int32_t depth, int32_t precision, uint32_t flags,
+                                 int32_t out_format, void* d_out, int32_t out_frame_rows,
+                                 uint64_t* d_segments, void* stream);
 
 /* ---- host helpers (restatements the host side of rt_scene needs) -------- */
 /* Camera::init (scene.cpp:80-106) in fp64: fills cam from the Camera fields.

@@ -89,9 +89,10 @@ struct rt_ctx {
         int32_t W = -1, row0 = -1, nrows = -1;
         unsigned long long scene_gen = 0;
         unsigned fb_epoch = 0;  // rt_set_option(RT_OPT_ROW_FEEDBACK) starts a new epoch
+        int32_t tstride = 0, tphase = 0;  // interleaved parts (KParams::tstride)
         bool operator==(const Band& o) const {
             return W == o.W && row0 == o.row0 && nrows == o.nrows && scene_gen == o.scene_gen &&
-                   fb_epoch == o.fb_epoch;
+                   fb_epoch == o.fb_epoch && tstride == o.tstride && tphase == o.tphase;
         }
     };
     unsigned fb_epoch = 0;  // a snapshot still in flight from an older epoch is not used
@@ -1222,7 +1223,7 @@ static int prepare_rows(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t
                         hipStream_t st, rt::KParams& p) {
     const int gy = (nrows + rt::TILE_H - 1) / rt::TILE_H;
     const int per_row = ((cam->width + rt::TILE_W - 1) / rt::TILE_W) * (rt::BLOCK / 64);
-    const rt_ctx::Band band{cam->width, row0, nrows, ctx->scene_gen, ctx->fb_epoch};
+    const rt_ctx::Band band{cam->width, row0, nrows, ctx->scene_gen, ctx->fb_epoch, p.tstride, p.tphase};
     if (ctx->cost_pending && hipEventQuery(ctx->ev_cost) == hipSuccess) {
         ctx->cost_pending = false;
         const rt_ctx::Band& b = ctx->cost_band;
@@ -1281,7 +1282,7 @@ static int prepare_rows(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t
 static int snapshot_costs(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nrows,
                           hipStream_t st, const rt::KParams& p) {
     if (!p.tile_cost) return RT_OK;
-    const rt_ctx::Band band{cam->width, row0, nrows, ctx->scene_gen, ctx->fb_epoch};
+    const rt_ctx::Band band{cam->width, row0, nrows, ctx->scene_gen, ctx->fb_epoch, p.tstride, p.tphase};
     const int gy = (nrows + rt::TILE_H - 1) / rt::TILE_H;
     const size_t n = (size_t)gy * ((cam->width + rt::TILE_W - 1) / rt::TILE_W) * (rt::BLOCK / 64);
     RT_HIP(ctx, hipMemcpyAsync(ctx->h_cost, ctx->d_cost, n * sizeof(uint16_t),
@@ -1293,9 +1294,20 @@ static int snapshot_costs(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32
     return RT_OK;
 }
 
-int rt_render_device(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nrows,
-                     int32_t depth, int32_t precision, uint32_t flags, int32_t out_format,
-                     void* d_out, uint64_t* d_segments, void* stream) {
+/* Pixel rows of interleaved part `part` of `nparts` (tile rows part, part + nparts, ...). */
+static int32_t interleaved_rows(int32_t height, int32_t nparts, int32_t part) {
+    const int32_t T = (height + rt::TILE_H - 1) / rt::TILE_H;
+    int32_t n = 0;
+    for (int32_t t = part; t < T; t += nparts) n += std::min(rt::TILE_H, height - t * rt::TILE_H);
+    return n;
+}
+
+/* rt_render_device and rt_render_device_interleaved: a contiguous band [row0, row0 + nrows)
+ * (nparts == 0) or interleaved part `part` of `nparts` (nrows = its pixel rows). */
+static int render_device_impl(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nrows,
+                              int32_t nparts, int32_t part, int32_t out_frame, int32_t depth,
+                              int32_t precision, uint32_t flags, int32_t out_format, void* d_out,
+                              uint64_t* d_segments, void* stream) {
 #if RT_HOST_PROFILE
     double hp_t = hp_now();
     g_hn++;
@@ -1308,8 +1320,22 @@ int rt_render_device(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nr
     DeviceGuard dg(ctx->device);
     RT_HIP(ctx, dg.err);
     HP(0);
-    rt::KParams p = make_params(ctx, cam, row0, nrows, depth, flags, out_format, d_out,
+    // an interleaved part's tile rows span the frame: its pixel boxes are the whole frame's
+    rt::KParams p = make_params(ctx, cam, nparts > 1 ? 0 : row0, nparts > 1 ? cam->height : nrows,
+                                depth, flags, out_format, d_out,
                                 reinterpret_cast<unsigned long long*>(d_segments));
+    if (nparts > 1) {
+        p.row0 = 0;
+        p.nrows = nrows;
+        p.tstride = nparts;
+        p.tphase = part;
+        p.frame_h = cam->height;
+        p.out_frame = out_frame ? 1 : 0;
+        p.pairs = 0;  // the two-pixel kernel is contiguous-only
+        // centre-out dispatch from the part's tile row nearest the frame's heavy row
+        const int nt = (nrows + rt::TILE_H - 1) / rt::TILE_H;
+        p.row_center = std::max(0, std::min(nt - 1, (p.row_center - part) / nparts));
+    }
     HP(1);
     void* s = stream ? stream : static_cast<void*>(ctx->stream);
     hipStream_t hs = static_cast<hipStream_t>(s);
@@ -1325,6 +1351,34 @@ int rt_render_device(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nr
     st = snapshot_costs(ctx, cam, row0, nrows, hs, p);
     HP(4);
     return st;
+}
+
+int rt_render_device(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nrows,
+                     int32_t depth, int32_t precision, uint32_t flags, int32_t out_format,
+                     void* d_out, uint64_t* d_segments, void* stream) {
+    return render_device_impl(ctx, cam, row0, nrows, 0, 0, 0, depth, precision, flags, out_format,
+                              d_out, d_segments, stream);
+}
+
+int rt_interleaved_rows(int32_t height, int32_t nparts, int32_t part, int32_t* nrows) {
+    if (!nrows || height < 0 || nparts <= 0 || part < 0 || part >= nparts) return RT_ERR_INVALID_ARG;
+    *nrows = interleaved_rows(height, nparts, part);
+    return RT_OK;
+}
+
+int rt_render_device_interleaved(rt_ctx* ctx, const rt_camera* cam, int32_t nparts, int32_t part,
+                                 int32_t depth, int32_t precision, uint32_t flags,
+                                 int32_t out_format, void* d_out, int32_t out_frame_rows,
+                                 uint64_t* d_segments, void* stream) {
+    if (!ctx || !cam || nparts <= 0 || part < 0 || part >= nparts || cam->height < 0)
+        return RT_ERR_INVALID_ARG;
+    if (nparts == 1)  // the whole frame: a contiguous band, stored at its frame rows anyway
+        return render_device_impl(ctx, cam, 0, cam->height, 0, 0, 0, depth, precision, flags,
+                                  out_format, d_out, d_segments, stream);
+    if (rt::TILE_H != 8) return RT_ERR_UNSUPPORTED;  // parts are dealt in 8-row tile rows
+    return render_device_impl(ctx, cam, 0, interleaved_rows(cam->height, nparts, part), nparts,
+                              part, out_frame_rows, depth, precision, flags, out_format, d_out,
+                              d_segments, stream);
 }
 
 int rt_render_device_frames(rt_ctx* ctx, const rt_camera* cams, int32_t ncams, int32_t row0,

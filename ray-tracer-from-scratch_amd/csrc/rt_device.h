@@ -197,6 +197,10 @@ struct KParams {
     float clu_cos;         // wide-cone waves (cone cos(half-angle) < clu_cos) use clusters
     float clu_oinf;        // rays whose |origin|inf exceeds it test every cluster (the box
                            // margin covers fp32 rounding only for origins near the scene)
+    // interleaved parts (rt_render_device_interleaved): tstride > 1 = the band is the
+    // frame's tile rows tphase, tphase + tstride, ... (nrows = their pixel rows, row0 = 0);
+    // frame_h = frame height; out_frame = store at frame rows instead of back to back
+    int32_t tstride, tphase, frame_h, out_frame;
 };
 // by-value kernel arguments of up to 16 KB arrive intact (tools/ubench/kernarg_size.hip,
 // kernarg_stale.hip: consistent across back-to-back launches)

@@ -70,6 +70,10 @@ struct Rank {
     hipEvent_t ev_rendered[RT_MULTI_SLOTS] = {nullptr, nullptr};
     hipEvent_t ev_sent[RT_MULTI_SLOTS] = {nullptr, nullptr};
     hipEvent_t ev_done = nullptr;   // root, RCCL: every band received
+    // root, RCCL, interleaved layout: every rank's part received here, then scattered into
+    // its frame rows (one strided copy per part)
+    void* staging[RT_MULTI_SLOTS] = {nullptr, nullptr};
+    size_t staging_cap = 0;
     // worker thread (local ranks other than the first, one process driving several GPUs)
     std::thread th;
     std::mutex mu;
@@ -84,6 +88,7 @@ struct Rank {
 
 struct rt_multi {
     int nranks = 1, nlocal = 1, first_rank = 0, transport = RT_TRANSPORT_RCCL;
+    int layout = 0;                 // RT_OPT_MULTI_LAYOUT: 0 contiguous bands, 1 interleaved
     std::vector<Rank*> r;           // local ranks, r[0] = first_rank
     uint64_t frame = 0;
     hipEvent_t ev_in[RT_MULTI_SLOTS] = {nullptr, nullptr};  // root's device (process with root)
@@ -177,6 +182,60 @@ int ensure_bands(rt_multi* m, Rank* k, size_t bytes) {
     return RT_OK;
 }
 
+/* A rank's rows of the frame: contiguous band (row0, nrows) or interleaved part (nrows). */
+struct Part {
+    int32_t row0 = 0, nrows = 0;
+};
+Part part_of(const rt_multi* m, int32_t height, int rank) {
+    Part pt;
+    if (m->layout == 1 && m->nranks > 1)
+        (void)rt_interleaved_rows(height, m->nranks, rank, &pt.nrows);
+    else
+        (void)rt_band_rows(height, m->nranks, rank, &pt.row0, &pt.nrows);
+    return pt;
+}
+/* Largest part of any rank (band buffer / staging size in rows). */
+int32_t max_part_rows(const rt_multi* m, int32_t height) {
+    int32_t mx = 0;
+    for (int g = 0; g < m->nranks; g++) mx = std::max(mx, part_of(m, height, g).nrows);
+    return mx;
+}
+/* Interleaved part `part` stored back to back at src -> its rows of the frame (tile rows of
+ * 8: a strided 2D copy of the full ones, then the frame's short last tile row if it is this
+ * part's). */
+int scatter_part(rt_multi* m, char* frame, const char* src, int32_t height, int part,
+                 size_t row_bytes, hipStream_t st) {
+    const int N = m->nranks, T = (height + 7) / 8;
+    if (part >= T || row_bytes == 0) return RT_OK;
+    const int nt = (T - part + N - 1) / N;
+    const bool partial = (height % 8) != 0 && ((T - 1) % N) == part;
+    const int nfull = nt - (partial ? 1 : 0);
+    if (nfull > 0)
+        MHIP(m, hipMemcpy2DAsync(frame + (size_t)part * 8 * row_bytes, (size_t)N * 8 * row_bytes, src,
+                                 8 * row_bytes, 8 * row_bytes, (size_t)nfull, hipMemcpyDefault, st));
+    if (partial)
+        MHIP(m, hipMemcpyAsync(frame + (size_t)(T - 1) * 8 * row_bytes, src + (size_t)nfull * 8 * row_bytes,
+                               (size_t)(height % 8) * row_bytes, hipMemcpyDefault, st));
+    return RT_OK;
+}
+/* A rank's rows rendered into `dst` on `st`: contiguous band -> dst + row0 rows (dst is the
+ * frame) or back to back (dst is a band buffer); interleaved part -> its frame rows
+ * (to_frame) or back to back. */
+int render_part(rt_multi* m, Rank* k, const Job& j, const Part& pt, char* dst, bool to_frame,
+                hipStream_t st) {
+    const rt_camera& cam = *j.cam;
+    const size_t row_bytes = (size_t)cam.width * bpp(j.out_format);
+    int e;
+    if (m->layout == 1 && m->nranks > 1)
+        e = rt_render_device_interleaved(k->ctx, &cam, m->nranks, k->rank, j.depth, j.precision,
+                                         j.flags, j.out_format, dst, to_frame ? 1 : 0, nullptr, st);
+    else
+        e = rt_render_device(k->ctx, &cam, pt.row0, pt.nrows, j.depth, j.precision, j.flags,
+                             j.out_format, to_frame ? dst + (size_t)pt.row0 * row_bytes : dst,
+                             nullptr, st);
+    return ctx_err(m, k, e, "rt_render_device");
+}
+
 /* One rank's share of one frame (see the file comment).  Runs on the caller's thread for
  * the first local rank and on the rank's worker thread for the others. */
 int enqueue_rank(rt_multi* m, Rank* k, const Job& j) {
@@ -184,50 +243,67 @@ int enqueue_rank(rt_multi* m, Rank* k, const Job& j) {
     MHIP(m, dg.err);
     const rt_camera& cam = *j.cam;
     const size_t row_bytes = (size_t)cam.width * bpp(j.out_format);
-    int32_t row0 = 0, nrows = 0;
-    int st = rt_band_rows(cam.height, m->nranks, k->rank, &row0, &nrows);
-    if (st != RT_OK) return st;
+    const bool inter = m->layout == 1 && m->nranks > 1;
+    const Part pt = part_of(m, cam.height, k->rank);
+    const int32_t nrows = pt.nrows;
+    int st = RT_OK;
     const int s = j.slot;
     if (k->rank == 0) {
-        // the root's band, in place, on the caller's stream
+        // the root's rows, in place in the frame, on the caller's stream
         if (nrows > 0) {
             SlowCall sc_("rt_render_device (root)");
-            st = rt_render_device(k->ctx, &cam, row0, nrows, j.depth, j.precision, j.flags,
-                                  j.out_format, j.d_frame + (size_t)row0 * row_bytes, nullptr,
-                                  j.stream);
-            if (st != RT_OK) return ctx_err(m, k, st, "rt_render_device");
+            st = render_part(m, k, j, pt, j.d_frame, true, j.stream);
+            if (st != RT_OK) return st;
         }
         if (m->transport == RT_TRANSPORT_RCCL && m->nranks > 1) {
+            const size_t part_bytes = (size_t)max_part_rows(m, cam.height) * row_bytes;
+            if (inter && part_bytes * m->nranks > k->staging_cap) {
+                // grow (rare): the comm stream may still scatter from the old buffers
+                MHIP(m, hipStreamSynchronize(k->comm_stream));
+                for (auto& b : k->staging) {
+                    if (b) MHIP(m, hipFree(b));
+                    b = nullptr;
+                }
+                k->staging_cap = 0;
+                for (auto& b : k->staging) MHIP(m, hipMalloc(&b, part_bytes * m->nranks));
+                k->staging_cap = part_bytes * m->nranks;
+            }
             MHIP(m, hipStreamWaitEvent(k->comm_stream, j.ev_in, 0));
             MNCCL(m, ncclGroupStart());
             for (int g = 1; g < m->nranks; g++) {
-                int32_t r0 = 0, nr = 0;
-                (void)rt_band_rows(cam.height, m->nranks, g, &r0, &nr);
-                if (nr <= 0 || row_bytes == 0) continue;
-                const ncclResult_t e = ncclRecv(j.d_frame + (size_t)r0 * row_bytes, (size_t)nr * row_bytes,
-                                                ncclUint8, g, k->comm, k->comm_stream);
+                const Part pg = part_of(m, cam.height, g);
+                if (pg.nrows <= 0 || row_bytes == 0) continue;
+                char* dst = inter ? static_cast<char*>(k->staging[s]) + (size_t)g * part_bytes
+                                  : j.d_frame + (size_t)pg.row0 * row_bytes;
+                const ncclResult_t e = ncclRecv(dst, (size_t)pg.nrows * row_bytes, ncclUint8, g,
+                                                k->comm, k->comm_stream);
                 if (e != ncclSuccess) {
                     (void)ncclGroupEnd();
                     return nccl_err(m, e, "ncclRecv");
                 }
             }
             MNCCL(m, ncclGroupEnd());
+            if (inter)
+                for (int g = 1; g < m->nranks; g++) {
+                    st = scatter_part(m, j.d_frame, static_cast<char*>(k->staging[s]) + (size_t)g * part_bytes,
+                                      cam.height, g, row_bytes, k->comm_stream);
+                    if (st != RT_OK) return st;
+                }
             MHIP(m, hipEventRecord(k->ev_done, k->comm_stream));
         }
         return RT_OK;
     }
     const size_t bytes = (size_t)nrows * row_bytes;
     if (bytes == 0) return RT_OK;  // an empty band (height < nranks): nothing to render or send
-    st = ensure_bands(m, k, (size_t)((cam.height + m->nranks - 1) / m->nranks) * row_bytes);
+    st = ensure_bands(m, k, (size_t)max_part_rows(m, cam.height) * row_bytes);
     if (st != RT_OK) return st;
     // band buffer `s` is free once the send of frame k - RT_MULTI_SLOTS has completed
     MHIP(m, hipStreamWaitEvent(k->render_stream[s], k->ev_sent[s], 0));
     {
         SlowCall sc_("rt_render_device (band)");
-        st = rt_render_device(k->ctx, &cam, row0, nrows, j.depth, j.precision, j.flags, j.out_format,
-                              k->band[s], nullptr, k->render_stream[s]);
+        st = render_part(m, k, j, pt, static_cast<char*>(k->band[s]), false, k->render_stream[s]);
     }
-    if (st != RT_OK) return ctx_err(m, k, st, "rt_render_device");
+    if (st != RT_OK) return st;
     MHIP(m, hipEventRecord(k->ev_rendered[s], k->render_stream[s]));
     MHIP(m, hipStreamWaitEvent(k->comm_stream, k->ev_rendered[s], 0));
     if (m->transport == RT_TRANSPORT_RCCL) {
@@ -235,8 +311,14 @@ int enqueue_rank(rt_multi* m, Rank* k, const Job& j) {
     } else {
         // the root's rows may still be read by the caller's earlier work on the frame buffer
         MHIP(m, hipStreamWaitEvent(k->comm_stream, j.ev_in, 0));
-        MHIP(m, hipMemcpyPeerAsync(j.d_frame + (size_t)row0 * row_bytes, m->r[0]->device, k->band[s],
-                                   k->device, bytes, k->comm_stream));
+        if (inter) {
+            st = scatter_part(m, j.d_frame, static_cast<const char*>(k->band[s]), cam.height, k->rank,
+                              row_bytes, k->comm_stream);
+            if (st != RT_OK) return st;
+        } else {
+            MHIP(m, hipMemcpyPeerAsync(j.d_frame + (size_t)pt.row0 * row_bytes, m->r[0]->device, k->band[s],
+                                       k->device, bytes, k->comm_stream));
+        }
     }
     MHIP(m, hipEventRecord(k->ev_sent[s], k->comm_stream));
     if (j.stream && m->transport == RT_TRANSPORT_RCCL && !m->has_root())
@@ -286,6 +368,8 @@ void destroy_rank(Rank* k) {
         if (k->ev_sent[s]) (void)hipEventDestroy(k->ev_sent[s]);
     }
     if (k->ev_done) (void)hipEventDestroy(k->ev_done);
+    for (auto& b : k->staging)
+        if (b) (void)hipFree(b);
     for (auto rs : k->render_stream)
         if (rs) (void)hipStreamDestroy(rs);
     if (k->comm_stream) (void)hipStreamDestroy(k->comm_stream);
@@ -529,6 +613,13 @@ int rt_multi_set_scene(rt_multi* m, const rt_prim* prims, int32_t n) {
 
 int rt_multi_set_option(rt_multi* m, int32_t option, int64_t value) {
     if (!m) return RT_ERR_INVALID_ARG;
+    if (option == RT_OPT_MULTI_LAYOUT) {
+        if (value != 0 && value != 1) return RT_ERR_INVALID_ARG;
+        const int st = rt_multi_sync(m);  // frames in flight keep the layout they started with
+        if (st != RT_OK) return st;
+        m->layout = (int)value;
+        return RT_OK;
+    }
     for (Rank* k : m->r) {
         const int st = rt_set_option(k->ctx, option, value);
         if (st != RT_OK) return ctx_err(m, k, st, "rt_set_option");

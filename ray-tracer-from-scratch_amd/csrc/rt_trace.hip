@@ -2153,6 +2153,31 @@ __device__ __forceinline__ int lane_mbcnt() {
     return (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
 }
 
+/* Rows of a band's tile row trow, sub-row sr (0..TILE_H-1): the frame row i it traces and
+ * whether it exists, and the output row it is stored at.  A contiguous band (tstride <= 1)
+ * is rows [row0, row0 + nrows), stored band-relative.  An interleaved part (KParams::tstride
+ * = nparts > 1, rt_render_device_interleaved) owns the frame's tile rows tphase, tphase +
+ * tstride, ...; it stores them back to back (band-relative) or, with out_frame, at their
+ * frame rows. */
+struct BandRow {
+    int i, out;
+    bool ok;
+};
+__device__ __forceinline__ BandRow band_row(const KParams& p, int trow, int sr) {
+    const int rloc = trow * TILE_H + sr;
+    BandRow b;
+    if (p.tstride > 1) {
+        b.i = (p.tphase + trow * p.tstride) * TILE_H + sr;
+        b.ok = b.i < p.frame_h;
+        b.out = p.out_frame ? b.i : rloc;
+    } else {
+        b.i = p.row0 + rloc;
+        b.ok = rloc < p.nrows;
+        b.out = rloc;
+    }
+    return b;
+}
+
 /* One tile per wave: tile column bx, tile row trow (after the row order), gx tile columns. */
 template <int PREC, bool SUN, bool INT_EXP, bool CULL, int MAXD>
 __device__ __forceinline__ void trace_tile(const KParams& p, int bx, int trow, int gx,
@@ -2163,20 +2188,21 @@ __device__ __forceinline__ void trace_tile(const KParams& p, int bx, int trow, i
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int x = bx * TILE_W + (TILE_W > 8 ? (wave & 1) * 8 : 0) + (lane & 7);
-    const int r = trow * TILE_H + (TILE_H > 8 ? (wave >> 1) * 8 : 0) + (lane >> 3);
-    const bool valid = x < p.W && r < p.nrows;
+    const BandRow br = band_row(p, trow, (TILE_H > 8 ? (wave >> 1) * 8 : 0) + (lane >> 3));
+    const bool valid = x < p.W && br.ok;
     uint64_t t_tile = 0;  // the wave's start stamp (taken inside trace_pixel_*)
-    const int i = p.row0 + r;
+    const int i = br.i;
     int segs = 0;
     // every lane runs the (converged) bounce loop; only valid lanes trace and store
     // the store's coordinates (see RT_STORE_RECOMPUTE)
     auto store = [&](double cr, double cg, double cb) __attribute__((always_inline)) {
         if (RT_STORE_RECOMPUTE && CULL && BLOCK == 64) {  // (linear kernels: no spill, A/B +1..12%)
             const int l2 = lane_mbcnt();
-            const int xs = bx * TILE_W + (l2 & 7), rs = trow * TILE_H + (l2 >> 3);
-            if (xs < p.W && rs < p.nrows) store_pixel(p, rs, xs, cr, cg, cb);
+            const int xs = bx * TILE_W + (l2 & 7);
+            const BandRow bs = band_row(p, trow, l2 >> 3);
+            if (xs < p.W && bs.ok) store_pixel(p, bs.out, xs, cr, cg, cb);
         } else if (valid) {
-            store_pixel(p, r, x, cr, cg, cb);
+            store_pixel(p, br.out, x, cr, cg, cb);
         }
     };
     if (PREC == PREC_F32) {

@@ -63,6 +63,7 @@ RT_OPT_PIXEL_PAIRS = 9
 RT_OPT_ROW_FEEDBACK_WARM = 10
 RT_OPT_WALL_ORDER = 11
 RT_OPT_CLUSTER_COS = 12
+RT_OPT_MULTI_LAYOUT = 13
 
 
 class rt_material(C.Structure):
@@ -136,6 +137,10 @@ SIGNATURES = [
     ("rt_selftest", C.c_int, [C.c_void_p, C.c_int32, C.c_uint64, C.c_uint64,
                               C.POINTER(C.c_uint64)]),
     ("rt_set_row_order", C.c_int, [C.c_void_p, C.POINTER(C.c_int16), C.c_int32]),
+    ("rt_interleaved_rows", C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_int32)]),
+    ("rt_render_device_interleaved", C.c_int,
+     [C.c_void_p, C.POINTER(rt_camera), C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_uint32,
+      C.c_int32, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]),
     # multi-GPU frame operator
     ("rt_multi_unique_id", C.c_int, [C.POINTER(C.c_uint8)]),
     ("rt_multi_create", C.c_int,
@@ -240,6 +245,23 @@ def band_rows(height: int, nranks: int, rank: int) -> tuple[int, int]:
     return r0.value, nr.value
 
 
+def interleaved_rows(height: int, nparts: int, part: int) -> int:
+    """rt_interleaved_rows: pixel rows of interleaved part `part` (tile rows part, part +
+    nparts, ... of 8 rows)."""
+    lib = load()
+    n = C.c_int32()
+    check(lib.rt_interleaved_rows(height, nparts, part, C.byref(n)))
+    return n.value
+
+
+def interleaved_row_index(height: int, nparts: int, part: int):
+    """Frame rows of interleaved part `part`, in the order the part stores them."""
+    rows = []
+    for t in range(part, (height + 7) // 8, nparts):
+        rows.extend(range(8 * t, min(8 * t + 8, height)))
+    return rows
+
+
 def out_dtype_shape(out_format: int, nrows: int, width: int):
     if out_format == RT_OUT_RGB_F32:
         return np.float32, (nrows, width, 3)
@@ -321,6 +343,17 @@ class Renderer:
                                         flags, out_format, C.c_void_p(d_out),
                                         C.c_void_p(d_segments or None),
                                         C.c_void_p(stream or None)), self.ctx)
+
+    def render_device_interleaved(self, cam: rt_camera, depth: int, nparts: int, part: int,
+                                  d_out: int, precision: int = RT_PREC_F64, flags: int = 0,
+                                  out_format: int = RT_OUT_RGB_F32, out_frame_rows: bool = False,
+                                  d_segments: int = 0, stream: int = 0) -> None:
+        """rt_render_device_interleaved: interleaved part `part` of `nparts` into device
+        memory, back to back (default) or at its frame rows."""
+        check(self.lib.rt_render_device_interleaved(
+            self.ctx, C.byref(cam), nparts, part, depth, precision, flags, out_format,
+            C.c_void_p(d_out), 1 if out_frame_rows else 0, C.c_void_p(d_segments or None),
+            C.c_void_p(stream or None)), self.ctx)
 
     def render_device_frames(self, cams, depth: int, d_outs, precision: int = RT_PREC_F64,
                              flags: int = 0, out_format: int = RT_OUT_RGB_F32, row0: int = 0,

@@ -139,3 +139,21 @@ def test_multi_args_rejected_without_device():
         capi.RT_ERR_INVALID_ARG
     assert lib.rt_multi_unique_id(None) == capi.RT_ERR_INVALID_ARG
     assert lib.rt_multi_last_error(None) == b""
+
+
+def test_interleaved_rows_partition():
+    """rt_interleaved_rows: the parts' tile rows (8 pixel rows, the frame's last one short)
+    cover every frame row exactly once; parts differ by at most one tile row."""
+    for h in (0, 1, 7, 8, 9, 36, 1080, 4321):
+        for n in (1, 2, 3, 4, 8):
+            rows = []
+            sizes = []
+            for p in range(n):
+                idx = capi.interleaved_row_index(h, n, p)
+                assert capi.interleaved_rows(h, n, p) == len(idx)
+                rows.extend(idx)
+                sizes.append(len(idx))
+            assert sorted(rows) == list(range(h))
+            assert max(sizes) - min(sizes) <= 8
+    with pytest.raises(capi.RTError):
+        capi.interleaved_rows(10, 2, 2)

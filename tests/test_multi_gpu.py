@@ -177,3 +177,70 @@ def test_create_errors():
     assert create([0], 2, 1, uid, capi.RT_TRANSPORT_COPY) == capi.RT_ERR_UNSUPPORTED
     assert create([0], 1, 1) == capi.RT_ERR_INVALID_ARG                # rank past nranks
     assert len(capi.multi_unique_id()) == capi.RT_MULTI_ID_BYTES
+
+
+@pytest.mark.parametrize("scene,w,h,depth", [("c2", 1920, 1080, 4), ("s64w6", 480, 270, 6),
+                                             ("s256w0", 203, 117, 8)])
+def test_interleaved_parts_bitwise(rend, scene, w, h, depth):
+    """rt_render_device_interleaved: every part of N in {2, 3, 8}, stored back to back and at
+    its frame rows, reassembles the one-GPU frame bitwise — linear-scan kernels (c2 scene)
+    and the cull kernels (64 and 256 spheres: wave cone, sphere clusters), ragged heights."""
+    import torch
+    dev = torch.device("cuda", 0)
+    sc = scenes.CONFIGS["c2"].scene() if scene == "c2" else \
+        scenes.synthetic_scene(int(scene[1:].split("w")[0]), int(scene.split("w")[1]))
+    prims = scenes.to_prims(sc)
+    rend.set_scene(prims)
+    cam = _cam(w, h)
+    ref, _ = rend.render(cam, depth, capi.RT_PREC_PATH64, 0, capi.RT_OUT_RGB_F32)
+    st = torch.cuda.Stream(dev)
+    for n in (2, 3, 8):
+        frame = torch.full((h, w, 3), -1.0, device=dev)
+        asm = np.full((h, w, 3), -1.0, np.float32)
+        for p in range(n):
+            rows = capi.interleaved_row_index(h, n, p)
+            band = torch.full((max(1, len(rows)), w, 3), -1.0, device=dev)
+            torch.cuda.synchronize()
+            rend.render_device_interleaved(cam, depth, n, p, band.data_ptr(), capi.RT_PREC_PATH64,
+                                           stream=st.cuda_stream)
+            rend.render_device_interleaved(cam, depth, n, p, frame.data_ptr(), capi.RT_PREC_PATH64,
+                                           out_frame_rows=True, stream=st.cuda_stream)
+            torch.cuda.synchronize()
+            if rows:
+                asm[rows] = band.cpu().numpy()[:len(rows)]
+        assert np.array_equal(asm.view(np.uint32), ref.view(np.uint32)), (scene, n)
+        assert np.array_equal(frame.cpu().numpy().view(np.uint32), ref.view(np.uint32)), (scene, n)
+
+
+@pytest.mark.parametrize("n", [2, 3, 8])
+def test_multi_interleaved_layout_bitwise(rend, n):
+    """RT_OPT_MULTI_LAYOUT = 1 (interleaved tile rows): config 4's frame and a 256-sphere
+    cull scene gathered from n ranks (peer copies, strided into the frame rows) are bitwise
+    the one-GPU frames, in one call and as frames in flight; switching layouts between
+    frames keeps them exact."""
+    import torch
+    dev = torch.device("cuda", 0)
+    cases = [(scenes.CONFIGS["c2"].scene(), 1920, 1080, 4),
+             (scenes.synthetic_scene(256, 0), 640, 360, 8)]
+    with capi.MultiRenderer([0] * n, transport=capi.RT_TRANSPORT_COPY) as m:
+        for sc, w, h, depth in cases:
+            prims = scenes.to_prims(sc)
+            rend.set_scene(prims)
+            m.set_scene(prims)
+            cam = _cam(w, h)
+            ref, _ = rend.render(cam, depth, capi.RT_PREC_PATH64, 0, capi.RT_OUT_RGB_F32)
+            for layout in (1, 0, 1):
+                m.set_option(capi.RT_OPT_MULTI_LAYOUT, layout)
+                got, _ = m.render(cam, depth, capi.RT_PREC_PATH64)
+                assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), (n, w, layout)
+            bufs = [torch.full((h, w, 3), -1.0, device=dev) for _ in range(2)]
+            sts = [torch.cuda.Stream(dev) for _ in range(2)]
+            torch.cuda.synchronize()
+            m.render_device_frames([cam], depth, [b.data_ptr() for b in bufs], capi.RT_PREC_PATH64,
+                                   streams=[s.cuda_stream for s in sts], nframes=5)
+            torch.cuda.synchronize()
+            m.sync()
+            for b in bufs:
+                assert np.array_equal(b.cpu().numpy().view(np.uint32), ref.view(np.uint32)), (n, w)
+        with pytest.raises(capi.RTError):
+            m.set_option(capi.RT_OPT_MULTI_LAYOUT, 2)
