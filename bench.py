@@ -155,6 +155,8 @@ def main() -> int:
     ap.add_argument("--sun", action="store_true", help="build-defined sun term (off = parity)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-c5", action="store_true",
+                    help="skip the config-5 side run (row-tiled 7680x4320 frames)")
     ap.add_argument("--no-sweep", action="store_true",
                     help="skip the side measurements (precision sweep, sun and moving-camera "
                          "loops, frame-sharded side run)")
@@ -511,6 +513,61 @@ def main() -> int:
                   "ms_per_step": round(float(t8.item()) / n8 * 1e3, 4),
                   "value": round(total_segs * n8 / float(t8.item()) / 1e6, 2), "unit": "Mrays/s"}
 
+    # ---- side run: BASELINE config 5 (7680x4320, 256 spheres, depth 8; the north_star's
+    # 8-GPU roofline run) through the same frame operator, row-tiled over the N ranks with
+    # the interleaved layout (tile rows dealt round-robin: the sphere cloud's heavy rows are
+    # shared; contiguous bands leave one rank 2.7x the average, tools/band_model.py) ----
+    c5 = None
+    if multi is not None and not args.no_sweep and args.config != "c5" and not args.no_c5:
+        c5cfg = scenes.CONFIGS["c5"]
+        c5sc = c5cfg.scene()
+        c5prims = scenes.to_prims(c5sc)
+        c5cam = capi.camera_init(**scenes.camera_args(c5cfg.width, c5cfg.height))
+        c5n = 8
+        multi.set_scene(c5prims)
+        rend.set_scene(c5prims)
+        layouts = (1, 0) if world > 1 else (0,)
+        c5 = {"workload": f"c5:{c5cfg.width}x{c5cfg.height}:d{c5cfg.depth}:s256w0",
+              "precision": args.precision, "frames": c5n}
+        # census of this rank's rows (interleaved parts: same total as any layout)
+        nr5 = capi.interleaved_rows(c5cfg.height, world, rank)
+        cbuf = torch.empty((max(1, nr5), c5cfg.width, 3), dtype=torch.float32, device=dev)
+        segs_t.zero_()
+        rend.render_device_interleaved(c5cam, c5cfg.depth, world, rank, cbuf.data_ptr(), prec,
+                                       d_segments=segs_t.data_ptr(), stream=stream.cuda_stream)
+        torch.cuda.synchronize(dev)
+        s5 = segs_t.clone()
+        if world > 1:
+            dist.all_reduce(s5, op=dist.ReduceOp.SUM)
+        c5segs = int(s5.item())
+        del cbuf
+        f5 = ([torch.empty((c5cfg.height, c5cfg.width, 3), dtype=torch.float32, device=dev)
+               for _ in range(2)] if multi.has_root else [])
+        p5 = [b.data_ptr() for b in f5]
+        sp5 = st_ptrs[:2] if multi.has_root else st_ptrs[:1]
+        for lay in layouts:
+            multi.set_option(capi.RT_OPT_MULTI_LAYOUT, lay)
+            multi.render_device_frames([c5cam], c5cfg.depth, p5, prec, flags, capi.RT_OUT_RGB_F32,
+                                       streams=sp5, nframes=2)
+            torch.cuda.synchronize(dev)
+            multi.sync()
+            barrier()
+            t50 = time.perf_counter()
+            multi.render_device_frames([c5cam], c5cfg.depth, p5, prec, flags, capi.RT_OUT_RGB_F32,
+                                       streams=sp5, nframes=c5n)
+            torch.cuda.synchronize(dev)
+            multi.sync()
+            barrier()
+            t5 = torch.tensor([time.perf_counter() - t50], dtype=torch.float64, device=dev)
+            if world > 1:
+                dist.all_reduce(t5, op=dist.ReduceOp.MAX)
+            name = "interleaved" if lay == 1 else ("contiguous" if world > 1 else "one GPU")
+            c5[name] = {"ms_per_frame": round(float(t5.item()) / c5n * 1e3, 3),
+                        "mrays_per_s": round(c5segs * c5n / float(t5.item()) / 1e6, 1)}
+        c5["segments_per_frame"] = c5segs
+        multi.set_option(capi.RT_OPT_MULTI_LAYOUT, 0)
+        del f5
+
     result = None
     if rank == 0:
         ms_step = elapsed_s / args.steps * 1e3
@@ -606,6 +663,7 @@ def main() -> int:
             "steady_state": steady,
             "frame_sharded": sharded,
             "tiled_rgba8": tiled8,
+            "c5_tiled": c5,
         }
         if world == 1 and not args.no_cpu_baseline and args.cpu_seconds > 0:
             result["cpu_baseline"] = cpu_baseline(cfg, prims, cam0, depth, flags, args.cpu_seconds)
