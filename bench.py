@@ -526,7 +526,7 @@ def main() -> int:
         c5n = 8
         multi.set_scene(c5prims)
         rend.set_scene(c5prims)
-        layouts = (1, 0) if world > 1 else (0,)
+        layouts = (1, 0) if multi.nranks > 1 else (0,)
         c5 = {"workload": f"c5:{c5cfg.width}x{c5cfg.height}:d{c5cfg.depth}:s256w0",
               "precision": args.precision, "frames": c5n}
         # census of this rank's rows (interleaved parts: same total as any layout)
@@ -561,7 +561,7 @@ def main() -> int:
             t5 = torch.tensor([time.perf_counter() - t50], dtype=torch.float64, device=dev)
             if world > 1:
                 dist.all_reduce(t5, op=dist.ReduceOp.MAX)
-            name = "interleaved" if lay == 1 else ("contiguous" if world > 1 else "one GPU")
+            name = "interleaved" if lay == 1 else ("contiguous" if multi.nranks > 1 else "one GPU")
             c5[name] = {"ms_per_frame": round(float(t5.item()) / c5n * 1e3, 3),
                         "mrays_per_s": round(c5segs * c5n / float(t5.item()) / 1e6, 1)}
         c5["segments_per_frame"] = c5segs

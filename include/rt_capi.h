@@ -196,6 +196,11 @@ enum rt_option {
                                          best hit skips its bounds test; 0 (default) = scene
                                          order (measured: c2 +1% with the order).  Output is
                                          identical (wall ties compare scene indices). */
+    RT_OPT_ROW_FEEDBACK_EMA = 14,     /* W in [0, 95] (default 0): the measured row order
+                                         ranks tile rows by their cost smoothed over the
+                                         band's snapshots, acc = W% acc + (100-W)% new;
+                                         0 = the latest snapshot alone.  Output is
+                                         identical. */
     RT_OPT_MULTI_LAYOUT = 13,         /* rt_multi_set_option only: 0 (default) = contiguous
                                          row bands (rt_band_rows); 1 = interleaved tile rows
                                          (rt_interleaved_rows): balanced when the frame's cost

@@ -100,6 +100,12 @@ struct rt_ctx {
     Band fb_band;                  // band fb_perm was computed for
     std::vector<int16_t> fb_perm;  // over dispatch units: 2^fb_units_log2 per tile row
     int fb_units_log2 = 0;
+    // RT_OPT_ROW_FEEDBACK_EMA: per-unit cost smoothed over the snapshots of one band
+    // (acc = w*acc + (1-w)*new), so one noisy snapshot (tile costs measured while another
+    // frame's waves shared the GPU) does not reorder the rows on its own; 0 = off
+    int fb_ema = 0;                // w in percent
+    std::vector<float> fb_acc;     // per dispatch unit, for fb_band
+
     int since_snapshot = 0;
     // RT_OPT_ROW_FEEDBACK_WARM: after a new band or scene, this many further snapshots are
     // taken back to back (each as soon as the previous one has landed) before the interval
@@ -1143,6 +1149,10 @@ int rt_set_option(rt_ctx* ctx, int32_t option, int64_t value) {
             if (value != 0 && value != 1) return RT_ERR_INVALID_ARG;
             ctx->pixel_pairs = value == 1;
             return RT_OK;
+        case RT_OPT_ROW_FEEDBACK_EMA:
+            if (value < 0 || value > 95) return RT_ERR_INVALID_ARG;
+            ctx->fb_ema = (int)value;
+            return RT_OK;
         case RT_OPT_ROW_FEEDBACK_WARM:
             if (value < 0 || value > 1000) return RT_ERR_INVALID_ARG;
             ctx->fb_warm = (int)value;
@@ -1204,7 +1214,8 @@ static int units_log2(int gy, int gx) {
 
 /* Dispatch units ordered by their most expensive wave (heaviest first; ties keep the lower
  * unit), from a cost snapshot of gy rows x gx tiles (one wave per tile). */
-static void order_units(const uint16_t* cost, int gy, int gx, int ul, std::vector<int16_t>& perm) {
+static void order_units(const uint16_t* cost, int gy, int gx, int ul, std::vector<int16_t>& perm,
+                        std::vector<float>& acc, bool acc_valid, int ema) {
     const int upr = 1 << ul, U = (gx + upr - 1) >> ul, nu = gy << ul;
     std::vector<uint32_t> mx(nu, 0);
     for (int r = 0; r < gy; r++)
@@ -1212,9 +1223,17 @@ static void order_units(const uint16_t* cost, int gy, int gx, int ul, std::vecto
             uint32_t& m = mx[(r << ul) + x / U];
             m = std::max<uint32_t>(m, cost[(size_t)r * gx + x]);
         }
+    // smoothed over the band's snapshots (RT_OPT_ROW_FEEDBACK_EMA), else this snapshot's
+    const float w = ema / 100.0f;
+    if (!acc_valid || (int)acc.size() != nu || ema <= 0) {
+        acc.assign(nu, 0.0f);
+        for (int u = 0; u < nu; u++) acc[u] = (float)mx[u];
+    } else {
+        for (int u = 0; u < nu; u++) acc[u] = w * acc[u] + (1.0f - w) * (float)mx[u];
+    }
     perm.resize(nu);
     for (int u = 0; u < nu; u++) perm[u] = (int16_t)u;
-    std::stable_sort(perm.begin(), perm.end(), [&](int16_t a, int16_t b) { return mx[a] > mx[b]; });
+    std::stable_sort(perm.begin(), perm.end(), [&](int16_t a, int16_t b) { return acc[a] > acc[b]; });
 }
 
 /* Before a launch: the row order (explicit, else the feedback's for this band) and the
@@ -1229,8 +1248,10 @@ static int prepare_rows(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t
         const rt_ctx::Band& b = ctx->cost_band;
         const int bgy = (b.nrows + rt::TILE_H - 1) / rt::TILE_H;
         const int bgx = ((b.W + rt::TILE_W - 1) / rt::TILE_W) * (rt::BLOCK / 64);
-        ctx->fb_units_log2 = units_log2(bgy, bgx);
-        order_units(ctx->h_cost, bgy, bgx, ctx->fb_units_log2, ctx->fb_perm);
+        const int ul = units_log2(bgy, bgx);
+        const bool same = ctx->fb_band == b && ctx->fb_units_log2 == ul;  // keep smoothing
+        ctx->fb_units_log2 = ul;
+        order_units(ctx->h_cost, bgy, bgx, ul, ctx->fb_perm, ctx->fb_acc, same, ctx->fb_ema);
         ctx->fb_band = b;
     }
     p.row_units_log2 = 0;

@@ -26,7 +26,13 @@ def main():
     r.set_option(capi.RT_OPT_BOX_CACHE, 0)
     r.set_option(capi.RT_OPT_ROW_FEEDBACK, fb)
     r.set_scene(prims)
-    m = capi.MultiRenderer([0])
+    ema = os.environ.get("EMA")
+    if ema is not None:   # A/B of the row-feedback smoothing: "multi" = a second plain ctx
+        r.set_option(capi.RT_OPT_ROW_FEEDBACK_EMA, 0)
+        m = capi.Renderer(0)
+        m.set_option(capi.RT_OPT_ROW_FEEDBACK_EMA, int(ema))
+    else:
+        m = capi.MultiRenderer([0])
     m.set_option(capi.RT_OPT_BOX_CACHE, 0)
     m.set_option(capi.RT_OPT_ROW_FEEDBACK, fb)
     m.set_scene(prims)
@@ -37,7 +43,9 @@ def main():
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(sts[0])
         sts[1].wait_stream(sts[0])
-        if which == "multi":
+        if which == "multi" and ema is not None:
+            m.render_device_frames([cam], cfg.depth, op, capi.RT_PREC_PATH64, streams=sp, nframes=n)
+        elif which == "multi":
             m.render_device_frames([cam], cfg.depth, op, capi.RT_PREC_PATH64, streams=sp, nframes=n)
         else:
             r.render_device_frames([cam], cfg.depth, op, capi.RT_PREC_PATH64, streams=sp, nframes=n)
@@ -52,7 +60,7 @@ def main():
     for _ in range(int(os.environ.get("ROUNDS", "6"))):
         for w in ("multi", "plain"):
             res[w].append(round(run(w), 2))
-    print(json.dumps({"row_feedback": fb, "us_per_frame": res, "median": {k: sorted(v)[len(v) // 2] for k, v in res.items()}}))
+    print(json.dumps({"row_feedback": fb, "ema_b": ema, "us_per_frame": res, "median": {k: sorted(v)[len(v) // 2] for k, v in res.items()}}))
 
 
 if __name__ == "__main__":
