@@ -5,7 +5,9 @@ one-stream kernel time (its own ctx, measured row order warm, HIP events around
 back-to-back launches), its host time per frame (rt_render_device with the GPU held busy),
 and the bytes it sends to the root.  The gather term needs the xGMI link rate, which one
 GPU cannot measure: the model takes it as a parameter.
-    python tools/band_model.py [--config c2] [--precision path64]"""
+With --layout interleaved the parts are rt_interleaved_rows parts (tile rows dealt
+round-robin, rt_render_device_interleaved), launched one at a time behind a GPU spin.
+    python tools/band_model.py [--config c2] [--precision path64] [--layout contiguous]"""
 import argparse
 import json
 import os
@@ -17,11 +19,45 @@ sys.path.insert(0, os.path.join(REPO, "ray-tracer-from-scratch_amd"))
 from rtamd import capi, scenes  # noqa: E402
 
 
+def interleaved_part(capi, torch, st, cam, depth, prec, prims, out, segs, N, r, n):
+    """One interleaved part's kernel / host time per frame and the bytes it sends."""
+    W = cam.width
+    nr = capi.interleaved_rows(cam.height, N, r)
+    rend = capi.Renderer(0)
+    rend.set_scene(prims)
+
+    def launch(d_seg=0):
+        rend.render_device_interleaved(cam, depth, N, r, out.data_ptr(), prec,
+                                       d_segments=d_seg, stream=st.cuda_stream)
+    for _ in range(40):
+        launch()
+    segs.zero_()
+    launch(segs.data_ptr())
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(st):   # the launches queue behind the spin: e0..e1 is GPU time only
+        torch.cuda._sleep(int(2e8))
+    e0.record(st)
+    t0 = time.perf_counter()
+    for _ in range(n):
+        launch()
+    host_us = (time.perf_counter() - t0) / n * 1e6
+    e1.record(st)
+    torch.cuda.synchronize()
+    kms = e0.elapsed_time(e1) / n
+    rend.close()
+    return {"rank": r, "nrows": nr, "kernel_us": round(kms * 1e3, 2),
+            "host_us": round(host_us, 2), "segments": int(segs.item()),
+            "send_bytes_f32": 0 if r == 0 else nr * W * 12,
+            "send_bytes_rgba8": 0 if r == 0 else nr * W * 4}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c2")
     ap.add_argument("--precision", default="path64")
     ap.add_argument("--launches", type=int, default=100)
+    ap.add_argument("--layout", choices=("contiguous", "interleaved"), default="contiguous")
     args = ap.parse_args()
     import torch
     dev = torch.device("cuda", 0)
@@ -35,10 +71,15 @@ def main():
     segs = torch.zeros(1, dtype=torch.int64, device=dev)
     n = args.launches
     res = {"config": args.config, "precision": args.precision, "width": W, "height": H,
-           "splits": {}}
+           "layout": args.layout, "splits": {}}
+    inter = args.layout == "interleaved"
     for N in (1, 2, 4, 8):
         bands = []
         for r in range(N):
+            if inter:
+                bands.append(interleaved_part(capi, torch, st, cam, cfg.depth, prec, prims, out,
+                                              segs, N, r, n))
+                continue
             r0, nr = capi.band_rows(H, N, r)
             rend = capi.Renderer(0)
             rend.set_scene(prims)
