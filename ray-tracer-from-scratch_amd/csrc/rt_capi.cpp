@@ -760,7 +760,8 @@ int pack_scene(const rt_prim* prims, int32_t n, rt_ctx::SceneHost& sc) {
     }
     const size_t nclu = leaves.size();
     const size_t off_clu = align_up(off_wnn + nW * 4 * sizeof(double), 256);
-    const size_t off_csph = align_up(off_clu + nclu * sizeof(rt::Clu32), 256);
+    // room for a multiple of four cluster records (the kernels read the boxes four at a time)
+    const size_t off_csph = align_up(off_clu + ((nclu + 3) & ~(size_t)3) * sizeof(rt::Clu32), 256);
     const size_t off_cord = align_up(off_csph + nclu * rt::CLU_SIZE * sizeof(rt::CluSph), 256);
     const size_t total = align_up(off_cord + 8 * rt::CLU_MAX, 256) + 256;
     sc.bytes.assign(total, 0);

@@ -1094,24 +1094,101 @@ __device__ __forceinline__ int clu_bit(const Clu32& B, int oct, int c) {
     const uint32_t hi = *reinterpret_cast<const uint32_t*>(B.rank + 4);
     return (int)(((oct < 4 ? lo : hi) >> (8 * (oct & 3))) & 0xff);
 }
-__device__ __forceinline__ float slab_t(const Clu32& B, const f3 o, const f3 inv) {
-    const float x1 = (B.lo[0] - o.x) * inv.x, x2 = (B.hi[0] - o.x) * inv.x;
-    const float y1 = (B.lo[1] - o.y) * inv.y, y2 = (B.hi[1] - o.y) * inv.y;
-    const float z1 = (B.lo[2] - o.z) * inv.z, z2 = (B.hi[2] - o.z) * inv.z;
-    const float tn = fmaxf(fmaxf(fminf(x1, x2), fminf(y1, y2)), fmaxf(fminf(z1, z2), 0.0f));
-    const float tf = fminf(fminf(fmaxf(x1, x2), fmaxf(y1, y2)), fmaxf(z1, z2));
+#ifndef RT_CLU_FAST  // 1: the cluster box pass RT_CLU_UNROLL boxes per iteration (scalar loads in one
+#define RT_CLU_FAST 1  // batch), slab planes as one fma each, the octant rank by one v_perm_b32,
+#endif                 // a 32-bit candidate mask while nclu <= 32
+#ifndef RT_CLU_UNROLL
+#define RT_CLU_UNROLL 2
+#endif
+#ifndef RT_CLU_SCHED
+#define RT_CLU_SCHED 1
+#endif
+/* Slab planes: RT_CLU_FAST forms (lo - o) / d as fma(lo, 1/d, -o/d) with o/d rounded once
+ * per ray.  Its error along the ray, 2^-24 |o| |d| / |d_axis| per plane, scales with the
+ * same 1 / |d_axis| as the box margin's slack (margin |d| / |d_axis|), so for origins within
+ * clu_oinf (100 x the extent, margin 1e-3 x the extent) the widened box still contains the
+ * balls' slabs.  d_axis = 0: NaN plane terms drop out of the min / max (no constraint),
+ * which is conservative. */
+struct SlabRay {
+    f3 o, inv, oi;  // origin, 1/d, o/d (fma form)
+};
+__device__ __forceinline__ SlabRay slab_ray(const f3 o, const f3 d) {
+    SlabRay r;
+    r.o = o;
+    r.inv = F3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    r.oi = F3(o.x * r.inv.x, o.y * r.inv.y, o.z * r.inv.z);
+    return r;
+}
+__device__ __forceinline__ void slab_tt(const Clu32& B, const SlabRay& s, float& tn, float& tf) {
+    float x1, x2, y1, y2, z1, z2;
+    if (RT_CLU_FAST) {
+        x1 = fmaf(B.lo[0], s.inv.x, -s.oi.x), x2 = fmaf(B.hi[0], s.inv.x, -s.oi.x);
+        y1 = fmaf(B.lo[1], s.inv.y, -s.oi.y), y2 = fmaf(B.hi[1], s.inv.y, -s.oi.y);
+        z1 = fmaf(B.lo[2], s.inv.z, -s.oi.z), z2 = fmaf(B.hi[2], s.inv.z, -s.oi.z);
+    } else {
+        x1 = (B.lo[0] - s.o.x) * s.inv.x, x2 = (B.hi[0] - s.o.x) * s.inv.x;
+        y1 = (B.lo[1] - s.o.y) * s.inv.y, y2 = (B.hi[1] - s.o.y) * s.inv.y;
+        z1 = (B.lo[2] - s.o.z) * s.inv.z, z2 = (B.hi[2] - s.o.z) * s.inv.z;
+    }
+    tn = fmaxf(fmaxf(fminf(x1, x2), fminf(y1, y2)), fmaxf(fminf(z1, z2), 0.0f));
+    tf = fminf(fminf(fmaxf(x1, x2), fmaxf(y1, y2)), fmaxf(z1, z2));
+}
+__device__ __forceinline__ float slab_t(const Clu32& B, const SlabRay& s) {
+    float tn, tf;
+    slab_tt(B, s, tn, tf);
     return tn <= tf ? tn : __builtin_inff();
+}
+/* The lane's candidate clusters as a bit mask: bit k = the cluster at rank k of the lane's
+ * octant order (OCT) or cluster k, for the clusters whose box the lane's ray meets (every
+ * cluster when !near).  RT_CLU_FAST: RT_CLU_UNROLL boxes per iteration (the clusters array holds
+ * room for a multiple of four records; the rest are masked off by c < nclu). */
+template <bool OCT, bool WIDE>
+__device__ __forceinline__ uint64_t clusters_mask(const KParams& p, const SlabRay& s, bool alive,
+                                                  bool near, int oct) {
+    // rank of cluster c in the lane's octant order: byte `oct` of Clu32::rank
+    const uint32_t sel = (uint32_t)oct | 0x0c0c0c00u;  // v_perm_b32: byte 0 <- byte oct, rest 0
+    using M = typename std::conditional<WIDE, uint64_t, uint32_t>::type;
+    M cm = 0;
+    const int n4 = (p.nclu + 3) & ~3;
+    for (int c0 = 0; c0 < n4; c0 += RT_CLU_UNROLL) {
+        Clu32 Bs[RT_CLU_UNROLL];  // wave-uniform: one batch of scalar loads
+#pragma unroll
+        for (int u = 0; u < RT_CLU_UNROLL; ++u) Bs[u] = p.clu[c0 + u];
+#pragma unroll
+        for (int u = 0; u < RT_CLU_UNROLL; ++u) {
+            // one box at a time (a handful of VGPRs), not four interleaved
+            if (RT_CLU_SCHED) __builtin_amdgcn_sched_barrier(0);
+            const int c = c0 + u;
+            const Clu32& B = Bs[u];
+            float tn, tf;
+            slab_tt(B, s, tn, tf);
+            const bool in = alive && c < p.nclu && (!near || tn <= tf);
+            uint32_t bit = (uint32_t)c;
+            if (OCT) {
+                const uint32_t lo = *reinterpret_cast<const uint32_t*>(B.rank);
+                const uint32_t hi = *reinterpret_cast<const uint32_t*>(B.rank + 4);
+                bit = __builtin_amdgcn_perm(hi, lo, sel);
+            }
+            cm |= (M)in << bit;
+        }
+    }
+    return (uint64_t)cm;
 }
 __device__ __forceinline__ void clusters_scan(const KParams& p, const RayD& r, bool alive, HitD& h) {
     const f3 o = F3((float)r.o.x, (float)r.o.y, (float)r.o.z);
     const f3 d = F3((float)r.d.x, (float)r.d.y, (float)r.d.z);
-    const f3 inv = F3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const SlabRay sr = slab_ray(o, d);
     const bool near = fmax3abs(o.x, o.y, o.z) <= p.clu_oinf;
     const int oct = clu_octant(d);
     uint64_t cm = 0;  // bit k: the cluster at rank k of this lane's octant order
-    for (int c = 0; c < p.nclu; ++c) {  // wave-uniform: scalar loads of the box
-        const bool in = !near || slab_t(p.clu[c], o, inv) < __builtin_inff();
-        cm |= (uint64_t)(alive && in) << clu_bit<RT_CLU_OCT>(p.clu[c], oct, c);
+    if (RT_CLU_FAST) {
+        cm = p.nclu <= 32 ? clusters_mask<RT_CLU_OCT, false>(p, sr, alive, near, oct)
+                          : clusters_mask<RT_CLU_OCT, true>(p, sr, alive, near, oct);
+    } else {
+        for (int c = 0; c < p.nclu; ++c) {  // wave-uniform: scalar loads of the box
+            const bool in = !near || slab_t(p.clu[c], sr) < __builtin_inff();
+            cm |= (uint64_t)(alive && in) << clu_bit<RT_CLU_OCT>(p.clu[c], oct, c);
+        }
     }
     const float dax = p.clu_axis == 0 ? d.x : (p.clu_axis == 1 ? d.y : d.z);
     const bool rev = !RT_CLU_OCT && dax < 0.0f;
@@ -1120,7 +1197,7 @@ __device__ __forceinline__ void clusters_scan(const KParams& p, const RayD& r, b
             const int k = rev ? 63 - __builtin_clzll(cm) : __builtin_ctzll(cm);
             cm &= ~(1ull << k);
             const int c = RT_CLU_OCT ? (int)p.cord[oct * CLU_MAX + k] : k;
-            const float t = near ? slab_t(p.clu[c], o, inv) : 0.0f;
+            const float t = near ? slab_t(p.clu[c], sr) : 0.0f;
             if ((double)t * r.dlen * (1.0 - 1e-3) <= h.dist) {
                 const CluSph* cs = p.csph + c * CLU_SIZE;
 #pragma unroll
@@ -1237,7 +1314,7 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
     // push and holds 2-3 VGPRs per level for the whole bounce loop, which is what the deep
     // fp64 kernels spilled to scratch.  LDS: one ds_write per value per bounce, one read
     // per level in the unwind, [level][lane] so a wave's accesses are conflict-free.
-    constexpr bool LSTK = RT_STACK_LDS && CULL;
+    constexpr bool LSTK = RT_STACK_LDS >= 2 || (RT_STACK_LDS && CULL);  // 2: every kernel
     __shared__ CT lds_s[LSTK ? MAXD * BLOCK : 1];
     __shared__ CT lds_k[(LSTK && SUN) ? MAXD * BLOCK : 1];
     __shared__ int lds_m[LSTK ? MAXD * BLOCK : 1];
@@ -1778,13 +1855,18 @@ __device__ __forceinline__ void sphere_f(const float* S, int s, f3 o, f3 d, floa
 __device__ __forceinline__ void clusters_scan_f(const KParams& p, f3 o, f3 d, float a, float ra,
                                                 float rl, bool alive, float& best, float& bpt,
                                                 int& slot) {
-    const f3 inv = F3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const SlabRay sr = slab_ray(o, d);
     const bool near = fmax3abs(o.x, o.y, o.z) <= p.clu_oinf;
     const int oct = clu_octant(d);
     uint64_t cm = 0;
-    for (int c = 0; c < p.nclu; ++c) {
-        const bool in = !near || slab_t(p.clu[c], o, inv) < __builtin_inff();
-        cm |= (uint64_t)(alive && in) << clu_bit<RT_CLU_OCT_F32>(p.clu[c], oct, c);
+    if (RT_CLU_FAST) {
+        cm = p.nclu <= 32 ? clusters_mask<RT_CLU_OCT_F32, false>(p, sr, alive, near, oct)
+                          : clusters_mask<RT_CLU_OCT_F32, true>(p, sr, alive, near, oct);
+    } else {
+        for (int c = 0; c < p.nclu; ++c) {
+            const bool in = !near || slab_t(p.clu[c], sr) < __builtin_inff();
+            cm |= (uint64_t)(alive && in) << clu_bit<RT_CLU_OCT_F32>(p.clu[c], oct, c);
+        }
     }
     const float dax = p.clu_axis == 0 ? d.x : (p.clu_axis == 1 ? d.y : d.z);
     const bool rev = !RT_CLU_OCT_F32 && dax < 0.0f;
@@ -1794,7 +1876,7 @@ __device__ __forceinline__ void clusters_scan_f(const KParams& p, f3 o, f3 d, fl
             const int k = rev ? 63 - __builtin_clzll(cm) : __builtin_ctzll(cm);
             cm &= ~(1ull << k);
             const int c = RT_CLU_OCT_F32 ? (int)p.cord[oct * CLU_MAX + k] : k;
-            const float t = near ? slab_t(p.clu[c], o, inv) : 0.0f;
+            const float t = near ? slab_t(p.clu[c], sr) : 0.0f;
             if (t * dl * (1.0f - 1e-3f) <= best) {
                 const CluSph* cs = p.csph + c * CLU_SIZE;
 #pragma unroll
