@@ -1194,11 +1194,13 @@ __device__ __forceinline__ void clusters_scan(const KParams& p, const RayD& r, b
     const bool rev = !RT_CLU_OCT && dax < 0.0f;
     while (__any(cm != 0)) {
         if (cm != 0) {
+            DIAG(6);  // (diagnostic build) one walk step: lanes with a cluster left
             const int k = rev ? 63 - __builtin_clzll(cm) : __builtin_ctzll(cm);
             cm &= ~(1ull << k);
             const int c = RT_CLU_OCT ? (int)p.cord[oct * CLU_MAX + k] : k;
             const float t = near ? slab_t(p.clu[c], sr) : 0.0f;
             if ((double)t * r.dlen * (1.0 - 1e-3) <= h.dist) {
+                DIAG(14);  // (diagnostic build) lanes whose cluster is not pruned
                 const CluSph* cs = p.csph + c * CLU_SIZE;
 #pragma unroll
                 for (int k = 0; k < CLU_SIZE; ++k) {
@@ -1226,6 +1228,10 @@ __device__ __forceinline__ HitD scan_d(const KParams& p, const RayD& r, bool ali
         // (PATH64 only: in the fp64-colour kernels the extra code costs more than it saves,
         // A/B c3 F64 +40%)
         const bool clusters = RT_CLUSTERS && CLU && p.nclu > 0 && cn.cos_t < p.clu_cos;
+#if RT_DIAG
+        if (alive) DIAG(0);  // wave-level segments of the cull kernels (tools/diag_run.py --cull)
+        if (clusters && alive) DIAG(4);
+#endif
         if (clusters) clusters_scan(p, r, alive, h);
         for (int c0 = 0; !clusters && c0 < p.nS; c0 += 64) {
             float lb;
@@ -1239,6 +1245,7 @@ __device__ __forceinline__ HitD scan_d(const KParams& p, const RayD& r, bool ali
                 const double bound = (double)lane_f(lb, l);
                 // exact skip: the sphere's distance is >= bound > this lane's best
                 if (alive && bound <= h.dist) {
+                    DIAG(12);  // (diagnostic build) one cone survivor tested
                     const int sidx = c0 + l;
                     const float Sf[4] = {lane_f(rec.f[0], l), lane_f(rec.f[1], l),
                                          lane_f(rec.f[2], l), lane_f(rec.f[3], l)};

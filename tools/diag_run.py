@@ -18,17 +18,25 @@ from rtamd import capi, scenes  # noqa: E402
 NAMES = {0: "scan", 2: "sphere_hit_body", 4: "wall_sign_pass", 6: "wall_bounds_body",
          12: "bounce_scan_binned", 14: "bounce_scan_unbinned",
          8: "shade_nonterminal", 10: "terminal_f32"}
+# the cull kernels' counters (c3, c5: --cull)
+NAMES_CULL = {0: "cull_scan", 2: "sphere_hit_body", 4: "clusters_scan", 6: "cluster_walk_step",
+              14: "cluster_visit_unpruned", 12: "cone_survivor_test", 8: "shade_nonterminal",
+              10: "terminal_f32"}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--lib", required=True)
     ap.add_argument("--setups", default="c2:4:path64")
+    ap.add_argument("--cull", action="store_true", help="name the cull kernels' counters")
     args = ap.parse_args()
+    names = NAMES_CULL if args.cull else NAMES
     lib = capi.load(args.lib)
     lib.rt_diag_read.argtypes = [C.POINTER(C.c_ulonglong)]
     h = C.c_void_p()
     capi.check(lib.rt_ctx_create(0, C.byref(h)))
+    # the row feedback's sampled frames run the stamped build, which has no counters
+    capi.check(lib.rt_set_option(h, capi.RT_OPT_ROW_FEEDBACK, 0))
     buf = (C.c_ulonglong * 16)()
     for su in args.setups.split(","):
         name, depth, prec = su.split(":")
@@ -50,7 +58,7 @@ def main():
         lib.rt_diag_read(buf)
         waves = (w + 7) // 8 * ((hh + 7) // 8)
         r = {"setup": su, "segments": st.segments, "waves": waves}
-        for i, n in NAMES.items():
+        for i, n in names.items():
             r[n] = {"wave_entries_per_wave": round(buf[i] / waves, 3),
                     "lanes_per_entry": round(buf[i + 1] / max(buf[i], 1), 2)}
         print(json.dumps(r), flush=True)
