@@ -120,7 +120,7 @@ struct rt_ctx {
         unsigned long long scene_gen = 0;
         rt_camera cam{};
         int32_t row0 = 0, nrows = 0, wave_cull = 0, opts = 0;
-        int32_t nbox = 0, row_center = 0, mir_depth = 0;
+        int32_t nbox = 0, nwbox = 0, row_center = 0, mir_depth = 0;
         size_t nmbox = 0;
         rt::PrimBox box[rt::BIN_MAX_PRIMS];
         rt::PrimBox mbox[rt::MIR_MAX_BOXES];
@@ -321,7 +321,7 @@ struct BoxAcc {
 #endif
 /* Boxes of every primitive (material-slot order) for the camera P (origin P.o). */
 void boxes_for(const rt_ctx* ctx, const Proj& P, double dmax, int32_t width, int32_t row0,
-               int32_t nrows, rt::PrimBox* out) {
+               int32_t nrows, rt::PrimBox* out, bool spheres = true) {
     const double W = width, R0 = row0, R1 = row0 + nrows - 1;
     const rt::PrimBox all{-1, (int16_t)width, (int16_t)(row0 - 1), (int16_t)(row0 + nrows)};
     const rt::PrimBox none{1, 0, 1, 0};
@@ -346,7 +346,7 @@ void boxes_for(const rt_ctx* ctx, const Proj& P, double dmax, int32_t width, int
                  bb = dot3(P.r[1], P.r[1]), cc = dot3(P.r[2], P.r[2]);
     const double na = std::sqrt(aa);
 #endif
-    for (int s = 0; s < ctx->sc.nS; s++) {
+    for (int s = 0; s < (spheres ? ctx->sc.nS : 0); s++) {
         const double* S = &ctx->sc.h_sph[5 * s];
         const double r = S[4];
         const double v[3] = {S[0] - o[0], S[1] - o[1], S[2] - o[2]};
@@ -440,10 +440,13 @@ void boxes_for(const rt_ctx* ctx, const Proj& P, double dmax, int32_t width, int
 void frame_boxes(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nrows,
                  rt::KParams& p) {
     p.nbox = 0;
+    p.nwbox = 0;
     p.mir_depth = 0;
     const int np = ctx->sc.nS + ctx->sc.nW;
-    if (!ctx->tile_bins || p.wave_cull || np == 0 || np > rt::BIN_MAX_PRIMS || cam->width > 32000 ||
-        cam->height > 32000 || nrows <= 0 || cam->width <= 0)
+    const bool cull_walls = p.wave_cull && ctx->sc.nW > 0 && ctx->sc.nW < rt::BIN_MAX_PRIMS;
+    if (!ctx->tile_bins || (p.wave_cull && !cull_walls) || np == 0 ||
+        (!p.wave_cull && np > rt::BIN_MAX_PRIMS) || cam->width > 32000 || cam->height > 32000 ||
+        nrows <= 0 || cam->width <= 0)
         return;
     Proj P;
     if (!make_proj(cam, P)) return;
@@ -458,6 +461,14 @@ void frame_boxes(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t 
         dmax = std::fmax(dmax, std::sqrt(dot3(d, d)));
     }
     if (!(dmax > 0) || !std::isfinite(dmax)) return;
+    if (p.wave_cull) {
+        // scenes with the wave cull: the spheres keep the cone, the walls get boxes (box[w])
+        std::vector<rt::PrimBox> all(np);
+        boxes_for(ctx, P, dmax, cam->width, row0, nrows, all.data(), false);
+        for (int w = 0; w < ctx->sc.nW; w++) p.box[w] = all[ctx->sc.nS + w];
+        p.nwbox = ctx->sc.nW;
+        return;
+    }
     boxes_for(ctx, P, dmax, cam->width, row0, nrows, p.box);
     p.nbox = np;
     // dispatch order (rt_trace.hip tile_row): centre-out from the weighted median tile row
@@ -651,6 +662,7 @@ rt::KParams make_params(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, i
         bc.wave_cull == p.wave_cull && bc.opts == opts &&
         std::memcmp(&bc.cam, cam, sizeof(rt_camera)) == 0) {
         p.nbox = bc.nbox;
+        p.nwbox = bc.nwbox;
         p.row_center = bc.row_center;
         p.mir_depth = bc.mir_depth;
         std::memcpy(p.box, bc.box, sizeof p.box);
@@ -671,6 +683,7 @@ rt::KParams make_params(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, i
     bc.wave_cull = p.wave_cull;
     bc.opts = opts;
     bc.nbox = p.nbox;
+    bc.nwbox = p.nwbox;
     bc.row_center = p.row_center;
     bc.mir_depth = p.mir_depth;
     bc.nmbox = (size_t)nm;

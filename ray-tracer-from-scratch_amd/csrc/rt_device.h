@@ -177,7 +177,9 @@ struct KParams {
                                 // (u & (2^k - 1)) of ceil(tiles / 2^k) tiles)
     int32_t row_perm_n;         // dispatch units in row_perm (== the grid's rows), 0 = unused
     int16_t row_perm[ROW_PERM_MAX];  // dispatch order of tile rows (rt_trace.hip tile_row)
-    PrimBox box[BIN_MAX_PRIMS]; // material-slot order: spheres, then walls
+    PrimBox box[BIN_MAX_PRIMS]; // material-slot order: spheres, then walls (scenes with the
+                                // wave cull: the walls' boxes only, box[w] = wall w)
+    int32_t nwbox;              // wave-cull scenes: walls with a PrimBox in box[] (0 = off)
     int32_t mir_depth;          // wall-sequence levels with mirror boxes (0 = off)
     int32_t pairs;              // RT_OPT_PIXEL_PAIRS: PATH64 linear-scan frames trace two
                                 // pixels per lane (16x8 pixels per wave)

@@ -740,6 +740,52 @@ __device__ __forceinline__ void walls_d(const KParams& p, const RayD& r, const R
     }
 }
 
+/* Walls against the wave's cone (RT_CULL_WALL_CONE): lane w tests wall w's circumscribed
+ * ball (centre P + X len/2 + Y wid/2, radius half the diagonal: every point the exact test
+ * can accept — the rectangle, its bounds checked in fp64 to ~1e-15 — lies in it) exactly as
+ * cull_chunk tests a sphere, with the same margins; a wall whose inflated ball misses the
+ * cone is missed by every live ray.  nW <= 64, all lanes active. */
+__device__ __forceinline__ uint64_t wall_cone_mask(const KParams& p, const Cone& cn) {
+    const int w = (int)(threadIdx.x & 63);
+    bool keep = false;
+    if (w < p.nW) {
+        keep = true;
+        const Wall32& Wl = p.w32[w];
+        const float hl = 0.5f * Wl.len, hw = 0.5f * Wl.wid;
+        const f3 C = F3(fmaf(Wl.Y[0], hw, fmaf(Wl.X[0], hl, Wl.P[0])),
+                        fmaf(Wl.Y[1], hw, fmaf(Wl.X[1], hl, Wl.P[1])),
+                        fmaf(Wl.Y[2], hw, fmaf(Wl.X[2], hl, Wl.P[2])));
+        const float rad = fsqrt(fmaf(hl, hl, hw * hw)) * 1.0001f;
+        const f3 v = C - cn.apex;
+        const float L2 = fdot(v, v);
+        const float R = rad + cn.rho + 1e-4f * (1.0f + cn.scale + fmax3abs(C.x, C.y, C.z) + rad);
+        if (L2 > R * R) {
+            const float il = frsq(L2);
+            const float sa = fminf(R * il, 1.0f);
+            const float ca = fsqrt(fmaxf(0.0f, 1.0f - sa * sa));
+            const float cphi = fdot(cn.u, v) * il;
+            keep = cphi >= cn.cos_t * ca - cn.sin_t * sa - 1e-4f;
+        }
+    }
+    const uint64_t b = __ballot(keep);
+    return ((uint64_t)__builtin_amdgcn_readfirstlane((unsigned)(b >> 32)) << 32) |
+           __builtin_amdgcn_readfirstlane((unsigned)b);
+}
+
+/* The cull kernels' primary walls behind the wall pixel boxes (RT_CULL_WALL_BINS): only
+ * the walls whose box meets the wave's tile (wave-uniform mask, bit w = wall w), in index
+ * order as walls_d. */
+template <bool MIXED>
+__device__ __forceinline__ void walls_d_kept(const KParams& p, const RayD& r, const RayF& rf,
+                                             HitD& h, uint64_t wm) {
+    while (wm) {
+        const int w = __builtin_ctzll(wm);
+        wm &= wm - 1;
+        if (MIXED && wall_cull(p.w32[w], rf)) continue;
+        wall_exact<false>(p.w64[w], w, p, r, h);
+    }
+}
+
 /* Linear scan (no wave cull): groups of 4 spheres per scalar load.  EYE: the primary
  * segment, origin terms from the eye tables (rt_device.h). */
 template <bool MIXED, bool EYE>
@@ -1021,6 +1067,12 @@ __device__ __forceinline__ uint64_t box_load_primary(const KParams& p) {
     const uint64_t v = *reinterpret_cast<const uint64_t*>(p.box + l);
     return l < p.nbox ? v : 0x80007fff80007fffull;
 }
+/* The cull kernels' wall boxes (RT_CULL_WALL_BINS): p.box[0 .. nwbox-1] = walls 0.. */
+__device__ __forceinline__ uint64_t box_load_walls(const KParams& p) {
+    const int l = threadIdx.x & 63;
+    const uint64_t v = *reinterpret_cast<const uint64_t*>(p.box + l);
+    return l < p.nwbox ? v : 0x80007fff80007fffull;
+}
 __device__ __forceinline__ uint64_t box_keep(uint64_t raw, TileO t) {
     const int x0 = (int16_t)(raw & 0xffff), x1 = (int16_t)((raw >> 16) & 0xffff);
     const int i0 = (int16_t)((raw >> 32) & 0xffff), i1 = (int16_t)(raw >> 48);
@@ -1102,6 +1154,12 @@ __device__ __forceinline__ int clu_bit(const Clu32& B, int oct, int c) {
 #endif
 #ifndef RT_CLU_SCHED
 #define RT_CLU_SCHED 1
+#endif
+#ifndef RT_CULL_WALL_CONE  // 1: the cull kernels' bounce segments test only the walls whose
+#define RT_CULL_WALL_CONE 1 // circumscribed ball meets the wave's cone (wall_cone_mask)
+#endif
+#ifndef RT_CULL_WALL_BINS  // 1: the cull kernels' primary segment tests only the walls whose
+#define RT_CULL_WALL_BINS 1 // pixel box meets the tile (KParams::nwbox; spheres keep the cone)
 #endif
 /* Slab planes: RT_CLU_FAST forms (lo - o) / d as fma(lo, 1/d, -o/d) with o/d rounded once
  * per ray.  Its error along the ray, 2^-24 |o| |d| / |d_axis| per plane, scales with the
@@ -1221,9 +1279,21 @@ __device__ __forceinline__ HitD scan_d(const KParams& p, const RayD& r, bool ali
         // walls first: their distances then bound the sphere tests
         RayF rf;
         if (MIXED) rf = make_rayf(r);
-        if (RT_WALLS_FIRST && alive) walls_d<MIXED>(p, r, rf, h);
         const Cone cn = wave_cone(F3((float)r.o.x, (float)r.o.y, (float)r.o.z),
                                   F3((float)r.d.x, (float)r.d.y, (float)r.d.z), alive);
+        if (RT_WALLS_FIRST) {
+            uint64_t wm = ~0ull;  // walls to test (bit w = wall w; walls past 63: all)
+            if (RT_CULL_WALL_BINS && primary && binned)
+                wm = keep;  // the primary segment: the walls' pixel boxes
+            else if (RT_CULL_WALL_CONE && cn.on && p.nW > 0 && p.nW <= 64)
+                wm = wall_cone_mask(p, cn);  // the bounces: the wave's cone
+            if (alive) {
+                if (wm != ~0ull)
+                    walls_d_kept<MIXED>(p, r, rf, h, wm);
+                else
+                    walls_d<MIXED>(p, r, rf, h);
+            }
+        }
         // a wide cone (live rays pointing everywhere) culls little: each lane its own clusters
         // (PATH64 only: in the fp64-colour kernels the extra code costs more than it saves,
         // A/B c3 F64 +40%)
@@ -1281,8 +1351,11 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
     using CT = typename std::conditional<COLOR64, double, float>::type;
     const d3 cpos = ld3(p.pos);
     const d3 pc = (ld3(p.tl) + ld3(p.dx) * (double)x) + ld3(p.dy) * (double)i;  // main.cpp:132
-    const uint64_t braw = CULL ? 0 : (RT_EARLY_LOADS >= 2 ? braw_in
-                                   : RT_EARLY_LOADS ? box_load_primary(p) : box_load(p, p.box));
+    uint64_t braw = 0;
+    if (!CULL)
+        braw = RT_EARLY_LOADS >= 2 ? braw_in : RT_EARLY_LOADS ? box_load_primary(p) : box_load(p, p.box);
+    else if (RT_CULL_WALL_BINS && p.nwbox > 0)  // (wave-uniform: scenes with walls only)
+        braw = box_load_walls(p);
     // main.cpp:133-134 (direction not normalised); the sphere terms only where needed
     // (PATH64: the fp32 terminal segment needs none of them)
     constexpr bool LAZY = RT_LAZY_TERMS && !COLOR64 && !CULL && RT_TERMINAL_F32;
@@ -1296,8 +1369,13 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
     t_start = RT_STAMP ? __builtin_amdgcn_s_memtime() : 0;
     if (RT_BOX_SCHED_BARRIER) __builtin_amdgcn_sched_barrier(0);  // compare after ray gen
     const TileO tile = tile_origin(x, i);
-    uint64_t keep = CULL ? ~0ull : box_keep(braw, tile);  // all lanes active
-    if (p.nbox == 0) keep = ~0ull;
+    uint64_t keep = ~0ull;
+    if (!CULL) {
+        keep = box_keep(braw, tile);  // all lanes active
+        if (p.nbox == 0) keep = ~0ull;
+    } else if (RT_CULL_WALL_BINS && p.nwbox > 0) {  // (wave-uniform)
+        keep = box_keep(braw, tile);  // the walls' boxes (bit w = wall w)
+    }
     STAGE(6);
     if (SKYF) {
         if (keep == 0) {  // wave-uniform: every primary ray of the tile misses (tile bins)
@@ -1362,6 +1440,7 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
         uint64_t km = ~0ull;
         if (!CULL && k == 0 && p.nbox > 0) km = keep;
         if (!CULL && k >= 1 && k <= p.mir_depth) km = mirror_keep<MAXD>(p, alive, st_m, k, tile);
+        if (CULL && RT_CULL_WALL_BINS && k == 0) km = keep;  // ~0 when the walls have no boxes
         if (LAZY && !terms && (km & smask) != 0) {  // a sphere may be tested
             ray_terms(r);
             terms = true;
@@ -1976,6 +2055,9 @@ __device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, bool
 #else
     const uint64_t keep = (!CULL && p.nbox > 0) ? tile_keep(p, p.box, tile) : ~0ull;
 #endif
+    // the cull kernels' primary walls behind their pixel boxes (RT_CULL_WALL_BINS)
+    uint64_t wkeep = ~0ull;
+    if (CULL && RT_CULL_WALL_BINS && p.nwbox > 0) wkeep = box_keep(box_load_walls(p), tile);
     if (!CULL && RT_SKY_FAST && keep == 0) {
         // wave-uniform: every primary ray misses (tile bins): the loop's miss shading below,
         // operation for operation, without the loop
@@ -2019,8 +2101,13 @@ __device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, bool
                 walls_f(p, o, d, best, slot, p.nS >= 64 ? 0 : km >> p.nS);
             }
         } else if (CULL) {
-            if (RT_WALLS_FIRST && alive) walls_f(p, o, d, best, slot);
             const Cone cn = wave_cone(o, d, alive);
+            if (RT_WALLS_FIRST) {
+                uint64_t wm = k == 0 ? wkeep : ~0ull;
+                if (RT_CULL_WALL_CONE && k > 0 && cn.on && p.nW > 0 && p.nW <= 64)
+                    wm = wall_cone_mask(p, cn);
+                if (alive) walls_f(p, o, d, best, slot, wm);
+            }
             // wide cone: each lane its own sphere clusters (clusters_scan)
             const bool clusters = RT_CLUSTERS_F32 && p.nclu > 0 && cn.cos_t < p.clu_cos;
             if (clusters) clusters_scan_f(p, o, d, a, ra, rl, alive, best, bpt, slot);

@@ -602,6 +602,68 @@ def test_tile_bins_are_output_invariant(rend, prec):
         rend.set_option(capi.RT_OPT_WAVE_CULL_MIN_SPHERES, 24)
 
 
+@pytest.mark.parametrize("prec", [capi.RT_PREC_F64, capi.RT_PREC_MIXED, capi.RT_PREC_PATH64,
+                                  capi.RT_PREC_F32])
+def test_cull_wall_bins_are_output_invariant(rend, prec):
+    """Scenes that use the wave cull keep the cone for their spheres but give their walls
+    pixel boxes (KParams::nwbox, RT_CULL_WALL_BINS): the primary segment tests only the walls
+    whose box meets the tile, and the bounce segments only the walls whose circumscribed ball
+    meets the wave's cone (RT_CULL_WALL_CONE).  Frames with the boxes (RT_OPT_TILE_BINS 1),
+    without, and from the linear-scan kernels are bitwise identical, segment counts too —
+    random sphere clouds with up to 40 walls, walls through the camera, axis-aligned views,
+    ragged images, row bands."""
+    rng = np.random.default_rng(47)
+    rend.set_option(capi.RT_OPT_WAVE_CULL_MIN_SPHERES, 0)  # every scene takes the cull kernels
+    try:
+        for trial, (ns, nw) in enumerate([(24, 6), (64, 6), (30, 12), (8, 3), (70, 40), (3, 1),
+                                          (40, 20), (100, 6)]):
+            sc = scenes.synthetic_scene(ns, min(nw, 6), seed=int(rng.integers(1 << 30)))
+            pos = rng.uniform([-1, -3, -1], [5, 3, 2])
+            for k in range(nw - 6):
+                sc.append(_random_wall(rng, near=pos if k % 3 == 0 else None))
+            rend.set_scene(scenes.to_prims(sc))
+            vfov = float(rng.choice([20.0, 60.0, 90.0, 150.0]))
+            w = int(rng.choice([9, 64, 161, 320]))
+            aspect = float(rng.choice([1.0, 16 / 9, 4 / 3]))
+            look = pos + (np.array([1.0, 0.0, 0.0]) if trial % 4 == 3 else rng.normal(size=3))
+            cam = capi.camera_init(pos, look, (0, 0, -1), vfov, aspect, float(w))
+            if cam.height <= 0:
+                continue
+            depth = int(rng.integers(0, 7))
+            r0 = int(rng.integers(0, cam.height))
+            n = int(rng.integers(1, cam.height - r0 + 1))
+            imgs = []
+            for on in (1, 0):
+                rend.set_option(capi.RT_OPT_TILE_BINS, on)
+                img, st = rend.render(cam, depth, prec, 0, capi.RT_OUT_RGB_F64, count_segments=True,
+                                      row0=r0, nrows=n)
+                imgs.append((img, st.segments))
+            # and the linear scan (no cone: every wall and sphere tested, RT_CULL_WALL_CONE's
+            # bounce-segment wall cull included in the comparison)
+            rend.set_option(capi.RT_OPT_WAVE_CULL_MIN_SPHERES, 2**31 - 1)
+            rend.set_option(capi.RT_OPT_TILE_BINS, 0)
+            img, st = rend.render(cam, depth, prec, 0, capi.RT_OUT_RGB_F64, count_segments=True,
+                                  row0=r0, nrows=n)
+            imgs.append((img, st.segments))
+            rend.set_option(capi.RT_OPT_WAVE_CULL_MIN_SPHERES, 0)
+            for q in (1, 2):
+                assert imgs[0][1] == imgs[q][1], (trial, q)
+                assert np.array_equal(imgs[0][0].view(np.uint64), imgs[q][0].view(np.uint64)), (trial, q)
+        # the configs' own scene and view at a reduced size (c3: 64 spheres + 6 walls)
+        cfg = scenes.CONFIGS["c3"]
+        rend.set_scene(scenes.to_prims(cfg.scene()))
+        cam = capi.camera_init(**scenes.camera_args(640, 360))
+        imgs = []
+        for on in (1, 0):
+            rend.set_option(capi.RT_OPT_TILE_BINS, on)
+            imgs.append(rend.render(cam, cfg.depth, prec, 0, capi.RT_OUT_RGB_F64, count_segments=True))
+        assert imgs[0][1].segments == imgs[1][1].segments
+        assert np.array_equal(imgs[0][0].view(np.uint64), imgs[1][0].view(np.uint64))
+    finally:
+        rend.set_option(capi.RT_OPT_TILE_BINS, 1)
+        rend.set_option(capi.RT_OPT_WAVE_CULL_MIN_SPHERES, 24)
+
+
 @pytest.mark.parametrize("prec", [capi.RT_PREC_F64, capi.RT_PREC_PATH64])
 def test_wall_order_is_output_invariant(rend, prec):
     """RT_OPT_WALL_ORDER (the primary scan visits walls nearest to the camera first): the
