@@ -745,31 +745,34 @@ __device__ __forceinline__ void walls_d(const KParams& p, const RayD& r, const R
  * can accept — the rectangle, its bounds checked in fp64 to ~1e-15 — lies in it) exactly as
  * cull_chunk tests a sphere, with the same margins; a wall whose inflated ball misses the
  * cone is missed by every live ray.  nW <= 64, all lanes active. */
+/* May a ray of the cone meet ball(C, rad)?  cull_chunk's test and margins. */
+__device__ __forceinline__ bool cone_ball(const Cone& cn, const f3 C, float rad) {
+    const f3 v = C - cn.apex;
+    const float L2 = fdot(v, v);
+    const float R = rad + cn.rho + 1e-4f * (1.0f + cn.scale + fmax3abs(C.x, C.y, C.z) + rad);
+    if (!(L2 > R * R)) return true;  // apex inside the inflated ball (or NaN): keep
+    const float il = frsq(L2);
+    const float sa = fminf(R * il, 1.0f);
+    const float ca = fsqrt(fmaxf(0.0f, 1.0f - sa * sa));
+    const float cphi = fdot(cn.u, v) * il;
+    return cphi >= cn.cos_t * ca - cn.sin_t * sa - 1e-4f;
+}
+/* Wall w's circumscribed ball (fp32): the rectangle's centre and half its diagonal. */
+__device__ __forceinline__ bool cone_wall(const Cone& cn, const Wall32& Wl) {
+    const float hl = 0.5f * Wl.len, hw = 0.5f * Wl.wid;
+    const f3 C = F3(fmaf(Wl.Y[0], hw, fmaf(Wl.X[0], hl, Wl.P[0])),
+                    fmaf(Wl.Y[1], hw, fmaf(Wl.X[1], hl, Wl.P[1])),
+                    fmaf(Wl.Y[2], hw, fmaf(Wl.X[2], hl, Wl.P[2])));
+    return cone_ball(cn, C, fsqrt(fmaf(hl, hl, hw * hw)) * 1.0001f);
+}
+__device__ __forceinline__ uint64_t ballot_u(bool b) {
+    const uint64_t m = __ballot(b);
+    return ((uint64_t)__builtin_amdgcn_readfirstlane((unsigned)(m >> 32)) << 32) |
+           __builtin_amdgcn_readfirstlane((unsigned)m);
+}
 __device__ __forceinline__ uint64_t wall_cone_mask(const KParams& p, const Cone& cn) {
     const int w = (int)(threadIdx.x & 63);
-    bool keep = false;
-    if (w < p.nW) {
-        keep = true;
-        const Wall32& Wl = p.w32[w];
-        const float hl = 0.5f * Wl.len, hw = 0.5f * Wl.wid;
-        const f3 C = F3(fmaf(Wl.Y[0], hw, fmaf(Wl.X[0], hl, Wl.P[0])),
-                        fmaf(Wl.Y[1], hw, fmaf(Wl.X[1], hl, Wl.P[1])),
-                        fmaf(Wl.Y[2], hw, fmaf(Wl.X[2], hl, Wl.P[2])));
-        const float rad = fsqrt(fmaf(hl, hl, hw * hw)) * 1.0001f;
-        const f3 v = C - cn.apex;
-        const float L2 = fdot(v, v);
-        const float R = rad + cn.rho + 1e-4f * (1.0f + cn.scale + fmax3abs(C.x, C.y, C.z) + rad);
-        if (L2 > R * R) {
-            const float il = frsq(L2);
-            const float sa = fminf(R * il, 1.0f);
-            const float ca = fsqrt(fmaxf(0.0f, 1.0f - sa * sa));
-            const float cphi = fdot(cn.u, v) * il;
-            keep = cphi >= cn.cos_t * ca - cn.sin_t * sa - 1e-4f;
-        }
-    }
-    const uint64_t b = __ballot(keep);
-    return ((uint64_t)__builtin_amdgcn_readfirstlane((unsigned)(b >> 32)) << 32) |
-           __builtin_amdgcn_readfirstlane((unsigned)b);
+    return ballot_u(w < p.nW && cone_wall(cn, p.w32[w]));
 }
 
 /* The cull kernels' primary walls behind the wall pixel boxes (RT_CULL_WALL_BINS): only
