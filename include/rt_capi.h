@@ -207,13 +207,13 @@ enum rt_option {
                                          is concentrated in some rows (config 5).  The
                                          gathered frame is identical. */
     RT_OPT_CLUSTER_COS = 12           /* C in [-2000, 2000] (default 400): in scenes that use
-                                         the wave cull, a RT_PREC_PATH64 or RT_PREC_F32
-                                         wave (their cull kernels) whose live
+                                         the wave cull, a wave (any precision) whose live
                                          rays' cone has cos(half-angle) < C/1000 tests each
                                          lane's own ray against sphere clusters (boxes of
                                          <= 8 spheres) and runs the exact test on its own
-                                         clusters only; -2000 = never (measured: c5 -36%,
-                                         c3 -4..5% at 300-500).  Output is identical. */
+                                         clusters only; -2000 = never (measured: c5 PATH64
+                                         -36%, F64 -44%, c3 -4..15% at 300-500).  Output is
+                                         identical. */
 };
 int rt_set_option(rt_ctx* ctx, int32_t option, int64_t value);
 

@@ -91,6 +91,10 @@
 #ifndef RT_CLU_OCT_F32     // the same for the F32 kernels (A/B: c5 F32 +4.5%, PATH64 -2..2.5%)
 #define RT_CLU_OCT_F32 0
 #endif
+#ifndef RT_CLUSTERS_F64    // 1: the same for the fp64-colour (F64, MIXED) cull kernels (A/B:
+                           // c5 F64 -44%, MIXED -36%, c3 F64 -14.5%, MIXED -9%)
+#define RT_CLUSTERS_F64 1
+#endif
 #ifndef RT_CLUSTERS_F32    // 1: the same for the F32 cull kernels
 #define RT_CLUSTERS_F32 1
 #endif
@@ -1298,8 +1302,9 @@ __device__ __forceinline__ HitD scan_d(const KParams& p, const RayD& r, bool ali
             }
         }
         // a wide cone (live rays pointing everywhere) culls little: each lane its own clusters
-        // (PATH64 only: in the fp64-colour kernels the extra code costs more than it saves,
-        // A/B c3 F64 +40%)
+        // (every precision since round 3: with the recursion stack in LDS the fp64-colour
+        // kernels have the registers for it — A/B c5 F64 -44%, MIXED -36%, c3 -9..15%; in
+        // round 2 it cost c3 F64 +40%)
         const bool clusters = RT_CLUSTERS && CLU && p.nclu > 0 && cn.cos_t < p.clu_cos;
 #if RT_DIAG
         if (alive) DIAG(0);  // wave-level segments of the cull kernels (tools/diag_run.py --cull)
@@ -1454,7 +1459,7 @@ __device__ __forceinline__ d3 trace_pixel_d(const KParams& p, int x, int i, bool
             else DIAG(14);
         }
 #endif
-        const HitD h = scan_d<MIXED, CULL, !COLOR64>(p, r, alive, k == 0, km != ~0ull, km);
+        const HitD h = scan_d<MIXED, CULL, !COLOR64 || RT_CLUSTERS_F64>(p, r, alive, k == 0, km != ~0ull, km);
         if (k == 0) STAGE(2);
         const bool last = k >= p.depth || k >= MAXD;  // remaining_iterations <= 0 (main.cpp:105)
         if (LAZY && !terms && __any(alive && !last && h.slot >= 0)) {  // a reflection follows
