@@ -647,8 +647,15 @@ __device__ __forceinline__ Cone wave_cone(f3 o, f3 d, bool alive) {
  * live ray of the wave: |hit - o_i| >= |C - o_i| - r >= |C - apex| - rho - r. */
 struct SphRec {
     float f[4];   // fp32 {cx, cy, cz, r} of sphere c0 + lane
-    double d[4];  // fp64 {cx, cy, cz, r^2} (WANT64 only)
+    double d[4];  // fp64 {cx, cy, cz, r^2} (WANT64 && !RT_CULL_REC64_SCALAR only)
 };
+/* RT_CULL_REC64_SCALAR: the cull pass loads only the fp32 records (16 B per lane instead of
+ * 48: ~1.5% of the spheres survive the cone), and each survivor's fp64 record comes in
+ * afterwards by one wave-uniform scalar load (the index is a ballot bit) instead of eight
+ * v_readlane from the testing lane's registers. */
+#ifndef RT_CULL_REC64_SCALAR
+#define RT_CULL_REC64_SCALAR 1
+#endif
 template <bool WANT64>
 __device__ __forceinline__ uint64_t cull_chunk(const KParams& p, const Cone& cn, int c0,
                                                float* lb, SphRec& rec) {
@@ -660,7 +667,7 @@ __device__ __forceinline__ uint64_t cull_chunk(const KParams& p, const Cone& cn,
 #pragma unroll
         for (int k = 0; k < 4; ++k) rec.f[k] = p.s32[s >> 2].c[k][s & 3];
         const float* S = rec.f;
-        if (WANT64) {
+        if (WANT64 && !RT_CULL_REC64_SCALAR) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) rec.d[k] = p.s64[s >> 2].v[s & 3][k];
         }
@@ -1328,9 +1335,13 @@ __device__ __forceinline__ HitD scan_d(const KParams& p, const RayD& r, bool ali
                     const float Sf[4] = {lane_f(rec.f[0], l), lane_f(rec.f[1], l),
                                          lane_f(rec.f[2], l), lane_f(rec.f[3], l)};
                     if (!(MIXED && sphere_cull(Sf, rf))) {
-                        const double Sd[4] = {lane_d(rec.d[0], l), lane_d(rec.d[1], l),
-                                              lane_d(rec.d[2], l), lane_d(rec.d[3], l)};
-                        sphere_exact<false>(Sd, sidx, r, h, &p);
+                        if (RT_CULL_REC64_SCALAR) {
+                            sphere_exact<false>(p.s64[sidx >> 2].v[sidx & 3], sidx, r, h, &p);
+                        } else {
+                            const double Sd[4] = {lane_d(rec.d[0], l), lane_d(rec.d[1], l),
+                                                  lane_d(rec.d[2], l), lane_d(rec.d[3], l)};
+                            sphere_exact<false>(Sd, sidx, r, h, &p);
+                        }
                     }
                 }
             }
