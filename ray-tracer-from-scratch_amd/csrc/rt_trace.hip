@@ -642,6 +642,31 @@ __device__ __forceinline__ Cone wave_cone(f3 o, f3 d, bool alive) {
     return c;
 }
 
+/* The primary segment's cone (RT_EYE_CONE): every primary ray starts at the camera, so the
+ * apex is that shared origin (rho 0 — what wave_cone's box reductions return for equal
+ * origins, without them), the axis the sum of the first and last live lanes' directions
+ * (any axis is valid: the half-angle is measured against it), and one reduction remains:
+ * the widest live direction. */
+#ifndef RT_EYE_CONE
+#define RT_EYE_CONE 1
+#endif
+__device__ __forceinline__ Cone wave_cone_eye(f3 o, f3 d, bool alive) {
+    Cone c;
+    const uint64_t am = __ballot(alive);
+    const int l0 = am ? __builtin_ctzll(am) : 0;
+    const int l1 = am ? 63 - __builtin_clzll(am) : 0;
+    c.apex = F3(lane_f(o.x, l0), lane_f(o.y, l0), lane_f(o.z, l0));
+    c.rho = 0.0f;
+    c.scale = fmax3abs(c.apex.x, c.apex.y, c.apex.z);
+    const f3 dn = alive ? fnormalize(d) : F3(0.f, 0.f, 0.f);
+    c.u = fnormalize(F3(lane_f(dn.x, l0) + lane_f(dn.x, l1), lane_f(dn.y, l0) + lane_f(dn.y, l1),
+                        lane_f(dn.z, l0) + lane_f(dn.z, l1)));
+    c.cos_t = uni(wmin(alive ? fdot(c.u, dn) : 1.0f)) - 1e-4f;
+    c.sin_t = fsqrt(fmaxf(0.0f, 1.0f - c.cos_t * c.cos_t));
+    c.on = c.cos_t > 0.05f;
+    return c;
+}
+
 /* Cull pass over spheres [c0, c0+64): lane l tests sphere c0 + l.  Returns the ballot of
  * survivors; *lb receives (in lane l) a lower bound on sphere c0+l's hit distance for any
  * live ray of the wave: |hit - o_i| >= |C - o_i| - r >= |C - apex| - rho - r. */
@@ -1293,8 +1318,10 @@ __device__ __forceinline__ HitD scan_d(const KParams& p, const RayD& r, bool ali
         // walls first: their distances then bound the sphere tests
         RayF rf;
         if (MIXED) rf = make_rayf(r);
-        const Cone cn = wave_cone(F3((float)r.o.x, (float)r.o.y, (float)r.o.z),
-                                  F3((float)r.d.x, (float)r.d.y, (float)r.d.z), alive);
+        const f3 co = F3((float)r.o.x, (float)r.o.y, (float)r.o.z);
+        const f3 cd = F3((float)r.d.x, (float)r.d.y, (float)r.d.z);
+        const Cone cn = (RT_EYE_CONE && primary) ? wave_cone_eye(co, cd, alive)
+                                                 : wave_cone(co, cd, alive);
         if (RT_WALLS_FIRST) {
             uint64_t wm = ~0ull;  // walls to test (bit w = wall w; walls past 63: all)
             if (RT_CULL_WALL_BINS && primary && binned)
@@ -2120,7 +2147,8 @@ __device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, bool
                 walls_f(p, o, d, best, slot, p.nS >= 64 ? 0 : km >> p.nS);
             }
         } else if (CULL) {
-            const Cone cn = wave_cone(o, d, alive);
+            const Cone cn = (RT_EYE_CONE && k == 0) ? wave_cone_eye(o, d, alive)
+                                                    : wave_cone(o, d, alive);
             if (RT_WALLS_FIRST) {
                 uint64_t wm = k == 0 ? wkeep : ~0ull;
                 if (RT_CULL_WALL_CONE && k > 0 && cn.on && p.nW > 0 && p.nW <= 64)
