@@ -201,7 +201,13 @@ enum rt_option {
                                          band's snapshots, acc = W% acc + (100-W)% new;
                                          0 = the latest snapshot alone.  Output is
                                          identical. */
-    RT_OPT_MULTI_LAYOUT = 13,         /* rt_multi_set_option only: 0 (default) = contiguous
+    RT_OPT_ROW_FEEDBACK_ISOLATE = 15, /* 1 (default): a frame whose tile costs
+                                         RT_OPT_ROW_FEEDBACK samples runs alone on the GPU
+                                         (its stream waits for this ctx's frames on other
+                                         streams, and their next frames wait for it), so the
+                                         costs are not those of overlapping frames; 0 = it
+                                         overlaps like any frame.  Output is identical. */
+    RT_OPT_MULTI_LAYOUT = 13,        /* rt_multi_set_option only: 0 (default) = contiguous
                                          row bands (rt_band_rows); 1 = interleaved tile rows
                                          (rt_interleaved_rows): balanced when the frame's cost
                                          is concentrated in some rows (config 5).  The

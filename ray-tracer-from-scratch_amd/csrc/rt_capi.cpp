@@ -80,11 +80,23 @@ struct rt_ctx {
     // Only the dispatch order changes: every tile is traced once per frame either way.
     int feedback = 32;             // refresh interval in frames, 0 = off
     bool pixel_pairs = RT_PIXEL_PAIRS_DEFAULT;  // RT_OPT_PIXEL_PAIRS
-    uint16_t* d_cost = nullptr;    // device, d_cost_cap entries
-    uint16_t* h_cost = nullptr;    // pinned host snapshot
+    uint16_t* d_cost = nullptr;    // device, d_cost_cap entries (one per wave)
     size_t d_cost_cap = 0;
+    uint32_t* d_umax = nullptr;    // device, per dispatch unit: its most expensive wave
+    uint32_t* h_umax = nullptr;    // pinned host snapshot of d_umax
+    size_t umax_cap = 0;
+    int cost_ul = 0;               // units per tile row (log2) of the pending snapshot
     hipEvent_t ev_cost = nullptr;  // snapshot landed
     bool cost_pending = false;
+    // RT_OPT_ROW_FEEDBACK_ISOLATE (default 1): a sampled frame runs alone on the GPU — its
+    // stream waits for the other streams' latest frames, and each other stream's next frame
+    // waits for it — so its wave costs are not those of two frames sharing the CUs (frames
+    // in flight overlap a frame's tail with the next one's start, which inflated or hid the
+    // costs of the tiles dispatched first and could install a worse order for 32 frames)
+    bool fb_isolate = true;
+    hipEvent_t ev_iso = nullptr;         // recorded behind the sampled frame
+    bool iso_pending = false;
+    std::vector<hipStream_t> iso_seen;   // streams already ordered behind ev_iso
     struct Band {
         int32_t W = -1, row0 = -1, nrows = -1;
         unsigned long long scene_gen = 0;
@@ -1032,6 +1044,9 @@ int rt_ctx_create(int device, rt_ctx** out) {
         if ((e = hipEventCreateWithFlags(&ctx->ev_cost, hipEventDisableTiming)) != hipSuccess) {
             st = hip_fail(ctx, e, "hipEventCreate"); break;
         }
+        if ((e = hipEventCreateWithFlags(&ctx->ev_iso, hipEventDisableTiming)) != hipSuccess) {
+            st = hip_fail(ctx, e, "hipEventCreate"); break;
+        }
         if ((e = hipMalloc(&ctx->d_segs, sizeof(unsigned long long))) != hipSuccess) {
             st = hip_fail(ctx, e, "hipMalloc(segs)"); break;
         }
@@ -1062,8 +1077,10 @@ int rt_ctx_destroy(rt_ctx* ctx) {
     if (ctx->d_segs) (void)hipFree(ctx->d_segs);
     if (ctx->ev_cost) (void)hipEventSynchronize(ctx->ev_cost);
     if (ctx->d_cost) (void)hipFree(ctx->d_cost);
-    if (ctx->h_cost) (void)hipHostFree(ctx->h_cost);
+    if (ctx->d_umax) (void)hipFree(ctx->d_umax);
+    if (ctx->h_umax) (void)hipHostFree(ctx->h_umax);
     if (ctx->ev_cost) (void)hipEventDestroy(ctx->ev_cost);
+    if (ctx->ev_iso) (void)hipEventDestroy(ctx->ev_iso);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -1167,6 +1184,10 @@ int rt_set_option(rt_ctx* ctx, int32_t option, int64_t value) {
             if (value < 0 || value > 95) return RT_ERR_INVALID_ARG;
             ctx->fb_ema = (int)value;
             return RT_OK;
+        case RT_OPT_ROW_FEEDBACK_ISOLATE:
+            if (value != 0 && value != 1) return RT_ERR_INVALID_ARG;
+            ctx->fb_isolate = value == 1;
+            return RT_OK;
         case RT_OPT_ROW_FEEDBACK_WARM:
             if (value < 0 || value > 1000) return RT_ERR_INVALID_ARG;
             ctx->fb_warm = (int)value;
@@ -1227,27 +1248,33 @@ static int units_log2(int gy, int gx) {
 }
 
 /* Dispatch units ordered by their most expensive wave (heaviest first; ties keep the lower
- * unit), from a cost snapshot of gy rows x gx tiles (one wave per tile). */
-static void order_units(const uint16_t* cost, int gy, int gx, int ul, std::vector<int16_t>& perm,
+ * unit), from the per-unit maxima of a cost snapshot (k_unit_max).  Host work is O(nu):
+ * the keys are 16-bit (wave costs saturate at 65535), sorted by a stable two-pass radix
+ * sort — the comparison sort it replaces took ~100 us on the thread that enqueues frames,
+ * long enough to starve the GPU once per snapshot. */
+static void order_units(const uint32_t* umax, int nu, std::vector<int16_t>& perm,
                         std::vector<float>& acc, bool acc_valid, int ema) {
-    const int upr = 1 << ul, U = (gx + upr - 1) >> ul, nu = gy << ul;
-    std::vector<uint32_t> mx(nu, 0);
-    for (int r = 0; r < gy; r++)
-        for (int x = 0; x < gx; x++) {
-            uint32_t& m = mx[(r << ul) + x / U];
-            m = std::max<uint32_t>(m, cost[(size_t)r * gx + x]);
-        }
     // smoothed over the band's snapshots (RT_OPT_ROW_FEEDBACK_EMA), else this snapshot's
     const float w = ema / 100.0f;
-    if (!acc_valid || (int)acc.size() != nu || ema <= 0) {
-        acc.assign(nu, 0.0f);
-        for (int u = 0; u < nu; u++) acc[u] = (float)mx[u];
-    } else {
-        for (int u = 0; u < nu; u++) acc[u] = w * acc[u] + (1.0f - w) * (float)mx[u];
+    const bool smooth = acc_valid && (int)acc.size() == nu && ema > 0;
+    if (!smooth) acc.assign(nu, 0.0f);
+    std::vector<uint16_t> key(nu);
+    for (int u = 0; u < nu; u++) {
+        const float m = (float)std::min<uint32_t>(umax[u], 65535u);
+        const float a = smooth ? w * acc[u] + (1.0f - w) * m : m;
+        acc[u] = a;
+        key[u] = (uint16_t)(65535u - (uint32_t)std::min(a + 0.5f, 65535.0f));  // descending
     }
+    std::vector<int16_t> tmp(nu);
     perm.resize(nu);
     for (int u = 0; u < nu; u++) perm[u] = (int16_t)u;
-    std::stable_sort(perm.begin(), perm.end(), [&](int16_t a, int16_t b) { return acc[a] > acc[b]; });
+    for (int sh = 0; sh < 16; sh += 8) {
+        unsigned cnt[257] = {0};
+        for (int k = 0; k < nu; k++) cnt[((key[perm[k]] >> sh) & 255) + 1]++;
+        for (int b = 0; b < 256; b++) cnt[b + 1] += cnt[b];
+        for (int k = 0; k < nu; k++) tmp[cnt[(key[perm[k]] >> sh) & 255]++] = perm[k];
+        perm.swap(tmp);
+    }
 }
 
 /* Before a launch: the row order (explicit, else the feedback's for this band) and the
@@ -1259,13 +1286,13 @@ static int prepare_rows(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t
     const rt_ctx::Band band{cam->width, row0, nrows, ctx->scene_gen, ctx->fb_epoch, p.tstride, p.tphase};
     if (ctx->cost_pending && hipEventQuery(ctx->ev_cost) == hipSuccess) {
         ctx->cost_pending = false;
+        ctx->iso_pending = false;  // the sampled frame has finished: nothing left to order
         const rt_ctx::Band& b = ctx->cost_band;
         const int bgy = (b.nrows + rt::TILE_H - 1) / rt::TILE_H;
-        const int bgx = ((b.W + rt::TILE_W - 1) / rt::TILE_W) * (rt::BLOCK / 64);
-        const int ul = units_log2(bgy, bgx);
+        const int ul = ctx->cost_ul;
         const bool same = ctx->fb_band == b && ctx->fb_units_log2 == ul;  // keep smoothing
         ctx->fb_units_log2 = ul;
-        order_units(ctx->h_cost, bgy, bgx, ul, ctx->fb_perm, ctx->fb_acc, same, ctx->fb_ema);
+        order_units(ctx->h_umax, bgy << ul, ctx->fb_perm, ctx->fb_acc, same, ctx->fb_ema);
         ctx->fb_band = b;
     }
     p.row_units_log2 = 0;
@@ -1294,19 +1321,28 @@ static int prepare_rows(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t
         return RT_OK;
     }
     const size_t need = (size_t)gy * per_row;
-    if (need > ctx->d_cost_cap) {
+    const size_t nu = (size_t)gy << units_log2(gy, per_row);
+    if (need > ctx->d_cost_cap || nu > ctx->umax_cap) {
         // grow (rare): nothing in flight may still use the old buffers
         RT_HIP(ctx, hipStreamSynchronize(st));
+        const int ws = wait_inflight(ctx);
+        if (ws != RT_OK) return ws;
         if (ctx->cost_pending) RT_HIP(ctx, hipEventSynchronize(ctx->ev_cost));
         ctx->cost_pending = false;
+        const size_t cap = std::max(need, ctx->d_cost_cap), ucap = std::max<size_t>({nu, ctx->umax_cap, 64});
         if (ctx->d_cost) RT_HIP(ctx, hipFree(ctx->d_cost));
-        if (ctx->h_cost) RT_HIP(ctx, hipHostFree(ctx->h_cost));
+        if (ctx->d_umax) RT_HIP(ctx, hipFree(ctx->d_umax));
+        if (ctx->h_umax) RT_HIP(ctx, hipHostFree(ctx->h_umax));
         ctx->d_cost = nullptr;
-        ctx->h_cost = nullptr;
+        ctx->d_umax = nullptr;
+        ctx->h_umax = nullptr;
         ctx->d_cost_cap = 0;
-        RT_HIP(ctx, hipMalloc(&ctx->d_cost, need * sizeof(uint16_t)));
-        RT_HIP(ctx, hipHostMalloc(&ctx->h_cost, need * sizeof(uint16_t), hipHostMallocDefault));
-        ctx->d_cost_cap = need;
+        ctx->umax_cap = 0;
+        RT_HIP(ctx, hipMalloc(&ctx->d_cost, cap * sizeof(uint16_t)));
+        RT_HIP(ctx, hipMalloc(&ctx->d_umax, ucap * sizeof(uint32_t)));
+        RT_HIP(ctx, hipHostMalloc(&ctx->h_umax, ucap * sizeof(uint32_t), hipHostMallocDefault));
+        ctx->d_cost_cap = cap;
+        ctx->umax_cap = ucap;
     }
     p.tile_cost = ctx->d_cost;
     return RT_OK;
@@ -1319,13 +1355,45 @@ static int snapshot_costs(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32
     if (!p.tile_cost) return RT_OK;
     const rt_ctx::Band band{cam->width, row0, nrows, ctx->scene_gen, ctx->fb_epoch, p.tstride, p.tphase};
     const int gy = (nrows + rt::TILE_H - 1) / rt::TILE_H;
-    const size_t n = (size_t)gy * ((cam->width + rt::TILE_W - 1) / rt::TILE_W) * (rt::BLOCK / 64);
-    RT_HIP(ctx, hipMemcpyAsync(ctx->h_cost, ctx->d_cost, n * sizeof(uint16_t),
+    const int gx = ((cam->width + rt::TILE_W - 1) / rt::TILE_W) * (rt::BLOCK / 64);
+    const int ul = units_log2(gy, gx);
+    // per-unit maxima on the device, then nu words back (not every wave's cost)
+    const int e = rt::launch_unit_max(ctx->d_cost, gy, gx, ul, ctx->d_umax, st);
+    if (e != (int)hipSuccess) return hip_fail(ctx, (hipError_t)e, "launch k_unit_max");
+    RT_HIP(ctx, hipMemcpyAsync(ctx->h_umax, ctx->d_umax, ((size_t)gy << ul) * sizeof(uint32_t),
                                hipMemcpyDeviceToHost, st));
     RT_HIP(ctx, hipEventRecord(ctx->ev_cost, st));
     ctx->cost_pending = true;
     ctx->cost_band = band;
+    ctx->cost_ul = ul;
     ctx->since_snapshot = 0;
+    return RT_OK;
+}
+
+/* RT_OPT_ROW_FEEDBACK_ISOLATE: before a launch on `st` — a sampled frame first waits for
+ * this ctx's latest frame on every other stream; any other frame whose stream has not yet
+ * been ordered behind the pending sampled frame waits for it once.  Device-side waits only
+ * (the host never blocks); streams are the ones launch_event tracks. */
+static int isolate_before(rt_ctx* ctx, hipStream_t st, bool sampled) {
+    if (!ctx->fb_isolate) return RT_OK;
+    if (sampled) {
+        // (ctx->stream is not tracked: rt_render synchronises it before returning)
+        for (const auto& f : ctx->inflight)
+            if (f.stream != st) RT_HIP(ctx, hipStreamWaitEvent(st, f.ev, 0));
+        return RT_OK;
+    }
+    if (!ctx->iso_pending) return RT_OK;
+    for (hipStream_t s : ctx->iso_seen)
+        if (s == st) return RT_OK;
+    RT_HIP(ctx, hipStreamWaitEvent(st, ctx->ev_iso, 0));
+    ctx->iso_seen.push_back(st);
+    return RT_OK;
+}
+static int isolate_after(rt_ctx* ctx, hipStream_t st, bool sampled) {
+    if (!ctx->fb_isolate || !sampled) return RT_OK;
+    RT_HIP(ctx, hipEventRecord(ctx->ev_iso, st));
+    ctx->iso_pending = true;
+    ctx->iso_seen.assign(1, st);
     return RT_OK;
 }
 
@@ -1379,9 +1447,14 @@ static int render_device_impl(rt_ctx* ctx, const rt_camera* cam, int32_t row0, i
     hipEvent_t done = nullptr;
     st = launch_event(ctx, hs, &done);
     if (st != RT_OK) return st;
+    const bool sampled = p.tile_cost != nullptr;
+    st = isolate_before(ctx, hs, sampled);
+    if (st != RT_OK) return st;
     HP(2);
     const int e = rt::launch_trace(p, precision, s, done);
     if (e != (int)hipSuccess) return hip_fail(ctx, (hipError_t)e, "launch k_trace");
+    st = isolate_after(ctx, hs, sampled);
+    if (st != RT_OK) return st;
     HP(3);
     st = snapshot_costs(ctx, cam, row0, nrows, hs, p);
     HP(4);

@@ -219,6 +219,9 @@ int max_depth();
 // pow: > 128 ulp) to *d_bad.
 int launch_selftest(int which, uint64_t n, uint64_t seed, unsigned long long* d_bad,
                     void* stream);
+// Row feedback: umax[(r << ul) + q] = the largest of cost[r * gx + q * U ..] over dispatch
+// unit q of row r (U = ceil(gx / 2^ul)), for gy rows of gx wave costs.
+int launch_unit_max(const uint16_t* cost, int gy, int gx, int ul, uint32_t* umax, void* stream);
 
 }  // namespace rt
 

@@ -2727,6 +2727,33 @@ int launch_selftest_ns(int which, uint64_t n, uint64_t seed, unsigned long long*
                        which, n, seed, d_bad);
     return (int)hipGetLastError();
 }
+
+/* ------------------------------------------------------------------------ */
+/* row feedback: per dispatch unit, the most expensive wave of a sampled frame */
+/* ------------------------------------------------------------------------ */
+/* One wave per tile row: unit (r << ul) + q covers waves [q*U, min(gx, q*U + U)) of row r
+ * (gx waves per row, U = ceil(gx / 2^ul)), the same split as the kernel's dispatch units.
+ * The host then reads nu words instead of every wave's cost (rt_capi.cpp order_units). */
+__global__ void __launch_bounds__(64) k_unit_max(const uint16_t* __restrict__ cost, int gy, int gx,
+                                                 int ul, uint32_t* __restrict__ umax) {
+    const int r = blockIdx.x;
+    if (r >= gy) return;
+    const int upr = 1 << ul, U = (gx + upr - 1) >> ul;
+    for (int q = 0; q < upr; q++) {
+        const int x0 = q * U, x1 = min(gx, x0 + U);
+        uint32_t m = 0;
+        for (int x = x0 + (int)threadIdx.x; x < x1; x += 64) m = max(m, (uint32_t)cost[(size_t)r * gx + x]);
+        for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off, 64));
+        if (threadIdx.x == 0) umax[(r << ul) + q] = m;
+    }
+}
+
+int launch_unit_max_ns(const uint16_t* cost, int gy, int gx, int ul, uint32_t* umax, void* stream) {
+    if (gy <= 0 || gx <= 0) return (int)hipSuccess;
+    hipLaunchKernelGGL(k_unit_max, dim3(gy), dim3(64), 0, static_cast<hipStream_t>(stream), cost, gy,
+                       gx, ul, umax);
+    return (int)hipGetLastError();
+}
 #endif  // !RT_STAMP
 
 }  // namespace kno / kst
@@ -2745,6 +2772,9 @@ int max_depth() { return kno::max_depth_ns(); }
 int launch_selftest(int which, uint64_t n, uint64_t seed, unsigned long long* d_bad,
                     void* stream) {
     return kno::launch_selftest_ns(which, n, seed, d_bad, stream);
+}
+int launch_unit_max(const uint16_t* cost, int gy, int gx, int ul, uint32_t* umax, void* stream) {
+    return kno::launch_unit_max_ns(cost, gy, gx, ul, umax, stream);
 }
 #endif
 

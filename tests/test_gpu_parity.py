@@ -792,6 +792,39 @@ def test_render_device_frames_equals_per_frame_calls(rend):
         rend.render_device_frames(cams, 4, [], capi.RT_PREC_PATH64, nframes=1)
 
 
+def test_row_feedback_isolated_sampling_in_flight(rend):
+    """Row feedback on frames in flight (three caller streams, a snapshot every other
+    frame): with RT_OPT_ROW_FEEDBACK_ISOLATE on (default) the sampled frames are ordered
+    between their neighbours on the device, and every frame is still the same frame —
+    each buffer bitwise equal to a plain render, isolation on or off, for a full frame and
+    a ragged band (the snapshot's per-unit reduction k_unit_max covers both)."""
+    import torch
+    dev = torch.device("cuda", 0)
+    sc = scenes.synthetic_scene(8, 4)
+    rend.set_scene(scenes.to_prims(sc))
+    cam = capi.camera_init(**scenes.camera_args(200, 117))
+    try:
+        for r0, n in ((0, 117), (13, 71)):
+            rend.set_option(capi.RT_OPT_ROW_FEEDBACK, 0)
+            ref, _ = rend.render(cam, 4, capi.RT_PREC_PATH64, 0, capi.RT_OUT_RGB_F32, row0=r0, nrows=n)
+            for iso in (1, 0):
+                rend.set_option(capi.RT_OPT_ROW_FEEDBACK_ISOLATE, iso)
+                rend.set_option(capi.RT_OPT_ROW_FEEDBACK, 1)
+                outs = [torch.zeros((n, 200, 3), dtype=torch.float32, device=dev) for _ in range(3)]
+                sts = [torch.cuda.Stream(dev) for _ in range(3)]
+                rend.render_device_frames([cam], 4, [o.data_ptr() for o in outs], capi.RT_PREC_PATH64,
+                                          row0=r0, nrows=n, streams=[s.cuda_stream for s in sts],
+                                          nframes=24)
+                torch.cuda.synchronize()
+                for o in outs:
+                    assert np.array_equal(o.cpu().numpy().view(np.uint32), ref.view(np.uint32)), (r0, iso)
+        with pytest.raises(capi.RTError):
+            rend.set_option(capi.RT_OPT_ROW_FEEDBACK_ISOLATE, 2)
+    finally:
+        rend.set_option(capi.RT_OPT_ROW_FEEDBACK_ISOLATE, 1)
+        rend.set_option(capi.RT_OPT_ROW_FEEDBACK, 32)
+
+
 def _pair_ab(rend, cam, depth, flags=0, **kw):
     """(one pixel per lane, two pixels per lane) PATH64 frames + segment counts."""
     out = []

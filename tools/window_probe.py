@@ -1,0 +1,84 @@
+#!/usr/bin/env python3
+"""Distribution of the driver's timed window: W windows of K consecutive frames (bench.py's
+timed loop: frames in flight on F streams, one C-ABI call per window), each bracketed by a
+device synchronize, after a 200-frame warm loop — per window the wall-clock and stream-event
+ms/frame.  Several option sets run one after another in one process, each on a fresh
+renderer (--variants 'name:OPT=V,OPT=V;name2:...', option names without RT_OPT_).
+
+    python tools/window_probe.py --windows 30 --steps 20 --variants 'base:;iso0:ROW_FEEDBACK_ISOLATE=0'
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "ray-tracer-from-scratch_amd"))
+from rtamd import capi, scenes  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--precision", default="path64")
+    ap.add_argument("--windows", type=int, default=30)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--fif", type=int, default=2)
+    ap.add_argument("--warm", type=int, default=200)
+    ap.add_argument("--variants", default="base:")
+    args = ap.parse_args()
+    import torch
+    dev = torch.device("cuda", 0)
+    cfg = scenes.CONFIGS[args.config]
+    prims = scenes.to_prims(cfg.scene())
+    cam = capi.camera_init(**scenes.camera_args(cfg.width, cfg.height))
+    prec = capi.PRECISIONS[args.precision]
+    streams = [torch.cuda.Stream(dev) for _ in range(args.fif)]
+    sp = [s.cuda_stream for s in streams]
+    outs = [torch.empty((cam.height, cam.width, 3), device=dev) for _ in range(args.fif)]
+    ptrs = [o.data_ptr() for o in outs]
+    segs = torch.zeros(1, dtype=torch.int64, device=dev)
+    for spec in args.variants.split(";"):
+        name, _, opts = spec.partition(":")
+        r = capi.Renderer(0)
+        r.set_option(capi.RT_OPT_BOX_CACHE, 0)
+        for kv in filter(None, opts.split(",")):
+            k, v = kv.split("=")
+            r.set_option(getattr(capi, "RT_OPT_" + k), int(v))
+        r.set_scene(prims)
+        r.render_device(cam, cfg.depth, ptrs[0], prec, d_segments=segs.data_ptr(), stream=sp[0])
+        torch.cuda.synchronize()
+        nseg = int(segs.item())
+        r.render_device_frames([cam], cfg.depth, ptrs, prec, streams=sp, nframes=args.warm)
+        torch.cuda.synchronize()
+        wall, gpu = [], []
+        for _ in range(args.windows):
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            t0 = time.perf_counter()
+            e0.record(streams[0])
+            for s in streams[1:]:
+                s.wait_stream(streams[0])
+            r.render_device_frames([cam], cfg.depth, ptrs, prec, streams=sp, nframes=args.steps)
+            for s in streams[1:]:
+                streams[0].wait_stream(s)
+            e1.record(streams[0])
+            torch.cuda.synchronize()
+            wall.append((time.perf_counter() - t0) / args.steps * 1e3)
+            gpu.append(e0.elapsed_time(e1) / args.steps)
+        r.close()
+        q = sorted(wall)
+        res = {"variant": name, "options": opts, "config": cfg.name, "precision": args.precision,
+               "steps": args.steps, "fif": args.fif, "windows": args.windows,
+               "wall_ms_median": round(statistics.median(wall), 4), "wall_ms_min": round(q[0], 4),
+               "wall_ms_p90": round(q[int(0.9 * (len(q) - 1))], 4), "wall_ms_max": round(q[-1], 4),
+               "gpu_ms_median": round(statistics.median(gpu), 4),
+               "grays_median": round(nseg / (statistics.median(wall) * 1e-3) / 1e9, 1),
+               "wall_ms": [round(v, 4) for v in wall]}
+        print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
