@@ -151,5 +151,11 @@ struct RtSceneOptions {
 };
 void rt_scene_set_options(const RtSceneOptions& opts);
 RtSceneOptions rt_scene_get_options();
+/* Releases rt_scene's process-wide renderer (device memory, worker threads, the RCCL
+ * communicator of a row-tiled renderer); the next rt_scene call makes a new one.  It also
+ * runs from an atexit handler registered when the renderer is made — i.e. after the HIP
+ * and RCCL runtimes have initialised, so before their own teardown — never from a static
+ * destructor. */
+void rt_scene_shutdown();
 
 #endif

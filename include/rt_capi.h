@@ -276,16 +276,26 @@ int rt_render_device_frames(rt_ctx* ctx, const rt_camera* cams, int32_t ncams, i
  * bands may differ in height by one row, so no padding; RT_TRANSPORT_COPY (one process
  * only) copies each band into the root's frame with hipMemcpyPeerAsync and also accepts
  * the same device more than once (several ranks on one GPU: the orchestration without
- * RCCL, e.g. on a one-GPU machine).
+ * RCCL, e.g. on a one-GPU machine); RT_TRANSPORT_RCCL_LOOPBACK is RT_TRANSPORT_RCCL with
+ * the root's own band also sent through RCCL (a self ncclSend/ncclRecv pair in the same
+ * group as the other bands' receives) and a communicator even at one rank — so every RCCL
+ * call of the gather (ncclCommInitRank, the group, send/recv, ncclCommGetAsyncError)
+ * executes on a one-GPU machine; it costs one extra copy of the root's band.
  * Frames in flight: each non-root rank renders into one of RT_MULTI_SLOTS band buffers on
  * its render stream while the previous frame's band is still being sent on its comm stream;
  * a band buffer is reused only after its send has completed (device-side event waits; the
- * host never blocks in rt_multi_render_device*). */
+ * host never blocks in rt_multi_render_device*).
+ * Failures: a frame that fails on one rank after another rank may already have queued its
+ * part of the gather leaves the communicator out of step; the rt_multi is then broken —
+ * every later frame returns RT_ERR_COMM, rt_multi_sync aborts the communicator
+ * (ncclCommAbort) instead of waiting on receives that cannot complete, and
+ * rt_multi_destroy aborts instead of destroying. */
 #define RT_MULTI_ID_BYTES 128
 #define RT_MULTI_SLOTS 2
 enum rt_transport {
     RT_TRANSPORT_RCCL = 0,
-    RT_TRANSPORT_COPY = 1
+    RT_TRANSPORT_COPY = 1,
+    RT_TRANSPORT_RCCL_LOOPBACK = 2
 };
 typedef struct rt_multi rt_multi;
 
@@ -375,6 +385,9 @@ int rt_frame_boxes(const rt_prim* prims, int32_t n, const rt_camera* cam, int32_
 
 /* Largest depth the kernels are compiled for (depth 0..rt_max_depth()). */
 int32_t rt_max_depth(void);
+
+/* Pixel rows per tile row of the kernels (the unit rt_interleaved_rows deals, 8). */
+int32_t rt_tile_rows(void);
 
 /* ---- diagnostics -------------------------------------------------------- */
 /* Device self-test of the fp64 helpers the exact path relies on, over n seeded random

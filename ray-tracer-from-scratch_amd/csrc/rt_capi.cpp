@@ -974,6 +974,8 @@ int32_t rt_out_bytes_per_pixel(int32_t out_format) { return bytes_per_pixel(out_
 
 int32_t rt_max_depth(void) { return rt::max_depth(); }
 
+int32_t rt_tile_rows(void) { return rt::TILE_H; }
+
 int rt_band_rows(int32_t height, int32_t nranks, int32_t rank, int32_t* row0, int32_t* nrows) {
     if (!row0 || !nrows || height < 0 || nranks <= 0 || rank < 0 || rank >= nranks)
         return RT_ERR_INVALID_ARG;

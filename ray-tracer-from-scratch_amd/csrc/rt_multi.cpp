@@ -97,7 +97,14 @@ struct rt_multi {
     void* d_frame = nullptr;
     size_t d_frame_cap = 0;
     char last_err[320] = {0};
+    // a frame failed after some rank may have queued its part of the gather: the
+    // communicator is out of step (see rt_capi.h); `aborted` once ncclCommAbort has run
+    bool broken = false, aborted = false;
     bool has_root() const { return first_rank == 0; }
+    bool rccl() const { return transport != RT_TRANSPORT_COPY; }
+    bool loopback() const { return transport == RT_TRANSPORT_RCCL_LOOPBACK; }
+    // the frame goes through a communicator (several ranks, or the root's band to itself)
+    bool gathers() const { return rccl() && (nranks > 1 || loopback()); }
 };
 
 namespace {
@@ -201,21 +208,22 @@ int32_t max_part_rows(const rt_multi* m, int32_t height) {
     return mx;
 }
 /* Interleaved part `part` stored back to back at src -> its rows of the frame (tile rows of
- * 8: a strided 2D copy of the full ones, then the frame's short last tile row if it is this
- * part's). */
+ * TH = rt_tile_rows() pixel rows: a strided 2D copy of the full ones, then the frame's short
+ * last tile row if it is this part's). */
 int scatter_part(rt_multi* m, char* frame, const char* src, int32_t height, int part,
                  size_t row_bytes, hipStream_t st) {
-    const int N = m->nranks, T = (height + 7) / 8;
+    const int N = m->nranks, TH = rt_tile_rows(), T = (height + TH - 1) / TH;
     if (part >= T || row_bytes == 0) return RT_OK;
     const int nt = (T - part + N - 1) / N;
-    const bool partial = (height % 8) != 0 && ((T - 1) % N) == part;
+    const bool partial = (height % TH) != 0 && ((T - 1) % N) == part;
     const int nfull = nt - (partial ? 1 : 0);
+    const size_t tile_bytes = (size_t)TH * row_bytes;
     if (nfull > 0)
-        MHIP(m, hipMemcpy2DAsync(frame + (size_t)part * 8 * row_bytes, (size_t)N * 8 * row_bytes, src,
-                                 8 * row_bytes, 8 * row_bytes, (size_t)nfull, hipMemcpyDefault, st));
+        MHIP(m, hipMemcpy2DAsync(frame + (size_t)part * tile_bytes, (size_t)N * tile_bytes, src,
+                                 tile_bytes, tile_bytes, (size_t)nfull, hipMemcpyDefault, st));
     if (partial)
-        MHIP(m, hipMemcpyAsync(frame + (size_t)(T - 1) * 8 * row_bytes, src + (size_t)nfull * 8 * row_bytes,
-                               (size_t)(height % 8) * row_bytes, hipMemcpyDefault, st));
+        MHIP(m, hipMemcpyAsync(frame + (size_t)(T - 1) * tile_bytes, src + (size_t)nfull * tile_bytes,
+                               (size_t)(height % TH) * row_bytes, hipMemcpyDefault, st));
     return RT_OK;
 }
 /* A rank's rows rendered into `dst` on `st`: contiguous band -> dst + row0 rows (dst is the
@@ -249,13 +257,24 @@ int enqueue_rank(rt_multi* m, Rank* k, const Job& j) {
     int st = RT_OK;
     const int s = j.slot;
     if (k->rank == 0) {
-        // the root's rows, in place in the frame, on the caller's stream
-        if (nrows > 0) {
+        const bool lb = m->loopback() && nrows > 0 && row_bytes > 0;
+        if (lb) {
+            // RT_TRANSPORT_RCCL_LOOPBACK: the root's rows into its band slot on the caller's
+            // stream (once the slot's previous self-send has completed), sent to itself below
+            st = ensure_bands(m, k, (size_t)max_part_rows(m, cam.height) * row_bytes);
+            if (st != RT_OK) return st;
+            MHIP(m, hipStreamWaitEvent(j.stream, k->ev_sent[s], 0));
+            SlowCall sc_("rt_render_device (root, loopback)");
+            st = render_part(m, k, j, pt, static_cast<char*>(k->band[s]), false, j.stream);
+            if (st != RT_OK) return st;
+            MHIP(m, hipEventRecord(k->ev_rendered[s], j.stream));
+        } else if (nrows > 0) {
+            // the root's rows, in place in the frame, on the caller's stream
             SlowCall sc_("rt_render_device (root)");
             st = render_part(m, k, j, pt, j.d_frame, true, j.stream);
             if (st != RT_OK) return st;
         }
-        if (m->transport == RT_TRANSPORT_RCCL && m->nranks > 1) {
+        if (m->gathers()) {
             const size_t part_bytes = (size_t)max_part_rows(m, cam.height) * row_bytes;
             if (inter && part_bytes * m->nranks > k->staging_cap) {
                 // grow (rare): the comm stream may still scatter from the old buffers
@@ -269,7 +288,18 @@ int enqueue_rank(rt_multi* m, Rank* k, const Job& j) {
                 k->staging_cap = part_bytes * m->nranks;
             }
             MHIP(m, hipStreamWaitEvent(k->comm_stream, j.ev_in, 0));
+            if (lb) MHIP(m, hipStreamWaitEvent(k->comm_stream, k->ev_rendered[s], 0));
             MNCCL(m, ncclGroupStart());
+            if (lb) {
+                const size_t bytes = (size_t)nrows * row_bytes;
+                char* dst = inter ? static_cast<char*>(k->staging[s]) : j.d_frame + (size_t)pt.row0 * row_bytes;
+                ncclResult_t e = ncclSend(k->band[s], bytes, ncclUint8, 0, k->comm, k->comm_stream);
+                if (e == ncclSuccess) e = ncclRecv(dst, bytes, ncclUint8, 0, k->comm, k->comm_stream);
+                if (e != ncclSuccess) {
+                    (void)ncclGroupEnd();
+                    return nccl_err(m, e, "ncclSend/ncclRecv (root to itself)");
+                }
+            }
             for (int g = 1; g < m->nranks; g++) {
                 const Part pg = part_of(m, cam.height, g);
                 if (pg.nrows <= 0 || row_bytes == 0) continue;
@@ -284,12 +314,13 @@ int enqueue_rank(rt_multi* m, Rank* k, const Job& j) {
             }
             MNCCL(m, ncclGroupEnd());
             if (inter)
-                for (int g = 1; g < m->nranks; g++) {
+                for (int g = lb ? 0 : 1; g < m->nranks; g++) {
                     st = scatter_part(m, j.d_frame, static_cast<char*>(k->staging[s]) + (size_t)g * part_bytes,
                                       cam.height, g, row_bytes, k->comm_stream);
                     if (st != RT_OK) return st;
                 }
             MHIP(m, hipEventRecord(k->ev_done, k->comm_stream));
+            if (lb) MHIP(m, hipEventRecord(k->ev_sent[s], k->comm_stream));  // slot s free again
         }
         return RT_OK;
     }
@@ -306,7 +337,7 @@ int enqueue_rank(rt_multi* m, Rank* k, const Job& j) {
     if (st != RT_OK) return st;
     MHIP(m, hipEventRecord(k->ev_rendered[s], k->render_stream[s]));
     MHIP(m, hipStreamWaitEvent(k->comm_stream, k->ev_rendered[s], 0));
-    if (m->transport == RT_TRANSPORT_RCCL) {
+    if (m->rccl()) {
         MNCCL(m, ncclSend(k->band[s], bytes, ncclUint8, 0, k->comm, k->comm_stream));
     } else {
         // the root's rows may still be read by the caller's earlier work on the frame buffer
@@ -321,7 +352,7 @@ int enqueue_rank(rt_multi* m, Rank* k, const Job& j) {
         }
     }
     MHIP(m, hipEventRecord(k->ev_sent[s], k->comm_stream));
-    if (j.stream && m->transport == RT_TRANSPORT_RCCL && !m->has_root())
+    if (j.stream && m->rccl() && !m->has_root())
         MHIP(m, hipStreamWaitEvent(j.stream, k->ev_sent[s], 0));
     return RT_OK;
 }
@@ -347,7 +378,7 @@ void worker_main(rt_multi* m, Rank* k) {
     }
 }
 
-void destroy_rank(Rank* k) {
+void destroy_rank(Rank* k, bool abort_comm) {
     if (k->th.joinable()) {
         {
             std::lock_guard<std::mutex> lk(k->mu);
@@ -360,7 +391,7 @@ void destroy_rank(Rank* k) {
     for (auto rs : k->render_stream)
         if (rs) (void)hipStreamSynchronize(rs);
     if (k->comm_stream) (void)hipStreamSynchronize(k->comm_stream);
-    if (k->comm) (void)ncclCommDestroy(k->comm);
+    if (k->comm) (void)(abort_comm ? ncclCommAbort(k->comm) : ncclCommDestroy(k->comm));
     for (auto& b : k->band)
         if (b) (void)hipFree(b);
     for (int s = 0; s < RT_MULTI_SLOTS; s++) {
@@ -390,6 +421,11 @@ int check_args(const rt_multi* m, const rt_camera* cam, int32_t depth, int32_t p
 /* One frame of rt_multi_render_device (arguments already checked). */
 int render_frame(rt_multi* m, const rt_camera* cam, int32_t depth, int32_t precision, uint32_t flags,
                  int32_t out_format, void* d_frame, void* stream) {
+    if (m->broken) {
+        std::snprintf(m->last_err, sizeof m->last_err,
+                      "an earlier frame failed after the gather was queued: the communicator is out of step");
+        return RT_ERR_COMM;
+    }
     const int slot = (int)(m->frame % RT_MULTI_SLOTS);
     Job j;
     j.cam = cam;
@@ -408,7 +444,7 @@ int render_frame(rt_multi* m, const rt_camera* cam, int32_t depth, int32_t preci
         j.ev_in = m->ev_in[slot];
         // one rank: the band is the frame, rendered in place in stream order; nothing else
         // writes the frame buffer, so no event is needed (it costs host time every frame)
-        if (m->nranks > 1) MHIP(m, hipEventRecord(j.ev_in, j.stream));
+        if (m->nranks > 1 || m->gathers()) MHIP(m, hipEventRecord(j.ev_in, j.stream));
     } else {
         j.stream = static_cast<hipStream_t>(stream);
     }
@@ -433,12 +469,15 @@ int render_frame(rt_multi* m, const rt_camera* cam, int32_t depth, int32_t preci
         }
     }
     m->frame++;
-    if (st != RT_OK) return st;
-    if (root && m->nranks > 1) {
+    if (st != RT_OK) {
+        if (m->gathers()) m->broken = true;  // another rank may have queued its send/recv
+        return st;
+    }
+    if (root && (m->nranks > 1 || m->gathers())) {
         // the caller's stream sees the complete frame
         DevGuard dg(root->device);
         MHIP(m, dg.err);
-        if (m->transport == RT_TRANSPORT_RCCL) {
+        if (m->rccl()) {
             MHIP(m, hipStreamWaitEvent(j.stream, root->ev_done, 0));
         } else {
             for (int L = 1; L < m->nlocal; L++) MHIP(m, hipStreamWaitEvent(j.stream, m->r[L]->ev_sent[slot], 0));
@@ -468,7 +507,9 @@ int rt_multi_create(const int32_t* devices, int32_t nlocal, int32_t nranks, int3
     *out = nullptr;
     if (!devices || nlocal <= 0 || nranks <= 0 || first_rank < 0 || first_rank + nlocal > nranks)
         return RT_ERR_INVALID_ARG;
-    if (transport != RT_TRANSPORT_RCCL && transport != RT_TRANSPORT_COPY) return RT_ERR_INVALID_ARG;
+    if (transport != RT_TRANSPORT_RCCL && transport != RT_TRANSPORT_COPY &&
+        transport != RT_TRANSPORT_RCCL_LOOPBACK)
+        return RT_ERR_INVALID_ARG;
     const bool one_process = nlocal == nranks;
     if (!one_process && (!unique_id || transport == RT_TRANSPORT_COPY))
         return transport == RT_TRANSPORT_COPY ? RT_ERR_UNSUPPORTED : RT_ERR_INVALID_ARG;
@@ -476,7 +517,7 @@ int rt_multi_create(const int32_t* devices, int32_t nlocal, int32_t nranks, int3
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return RT_ERR_NO_DEVICE;
     for (int L = 0; L < nlocal; L++)
         if (devices[L] < 0 || devices[L] >= ndev) return RT_ERR_NO_DEVICE;
-    if (transport == RT_TRANSPORT_RCCL)
+    if (transport != RT_TRANSPORT_COPY)
         for (int a = 0; a < nlocal; a++)
             for (int b = a + 1; b < nlocal; b++)
                 if (devices[a] == devices[b]) return RT_ERR_UNSUPPORTED;  // RCCL: one rank per GPU
@@ -546,8 +587,9 @@ int rt_multi_create(const int32_t* devices, int32_t nlocal, int32_t nranks, int3
         }
     }
     // one rank: the band is the frame and nothing is exchanged, so no communicator (RCCL's
-    // init would only print its banner on stdout and start its proxy thread)
-    if (st == RT_OK && transport == RT_TRANSPORT_RCCL && nranks > 1) {
+    // init would only print its banner on stdout and start its proxy thread) — except for
+    // the loopback transport, whose root sends its band to itself
+    if (st == RT_OK && m->gathers()) {
         ncclUniqueId id;
         if (one_process && !unique_id) {
             if (ncclGetUniqueId(&id) != ncclSuccess) fail(nccl_err(m, ncclInternalError, "ncclGetUniqueId"));
@@ -587,9 +629,23 @@ int rt_multi_create(const int32_t* devices, int32_t nlocal, int32_t nranks, int3
     return RT_OK;
 }
 
+/* A broken rt_multi: abort every local communicator once (pending receives that can no
+ * longer complete are cancelled, so the streams can drain). */
+void abort_comms(rt_multi* m) {
+    if (m->aborted) return;
+    m->aborted = true;
+    for (Rank* k : m->r)
+        if (k->comm) {
+            DevGuard dg(k->device);
+            (void)ncclCommAbort(k->comm);
+            k->comm = nullptr;
+        }
+}
+
 int rt_multi_destroy(rt_multi* m) {
     if (!m) return RT_ERR_INVALID_ARG;
-    for (Rank* k : m->r) destroy_rank(k);
+    if (m->broken) abort_comms(m);
+    for (Rank* k : m->r) destroy_rank(k, m->broken);
     m->r.clear();
     // the root's device objects (every rank has been synchronised above)
     for (auto& e : m->ev_in)
@@ -615,6 +671,7 @@ int rt_multi_set_option(rt_multi* m, int32_t option, int64_t value) {
     if (!m) return RT_ERR_INVALID_ARG;
     if (option == RT_OPT_MULTI_LAYOUT) {
         if (value != 0 && value != 1) return RT_ERR_INVALID_ARG;
+        if (value == 1 && rt_tile_rows() != 8) return RT_ERR_UNSUPPORTED;  // parts of 8-row tile rows
         const int st = rt_multi_sync(m);  // frames in flight keep the layout they started with
         if (st != RT_OK) return st;
         m->layout = (int)value;
@@ -700,6 +757,16 @@ int rt_multi_render(rt_multi* m, const rt_camera* cam, int32_t depth, int32_t pr
 
 int rt_multi_sync(rt_multi* m) {
     if (!m) return RT_ERR_INVALID_ARG;
+    if (m->broken) {
+        abort_comms(m);
+        for (Rank* k : m->r) {
+            DevGuard dg(k->device);
+            for (auto rs : k->render_stream) (void)hipStreamSynchronize(rs);
+            (void)hipStreamSynchronize(k->comm_stream);
+        }
+        std::snprintf(m->last_err, sizeof m->last_err, "a frame failed after the gather was queued: communicator aborted");
+        return RT_ERR_COMM;
+    }
     for (Rank* k : m->r) {
         DevGuard dg(k->device);
         MHIP(m, dg.err);

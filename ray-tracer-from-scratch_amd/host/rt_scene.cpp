@@ -14,6 +14,7 @@
  * subclass that does not override pack()) throws std::invalid_argument before any device
  * work.
  */
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -36,15 +37,32 @@ struct Global {
     std::vector<double> staging;
     std::vector<rt_prim> uploaded;  // the scene on the device (re-uploaded only on change)
     bool uploaded_tiled = false;    // ... of the tiled (rt_multi) or the one-GPU renderer
-    ~Global() {
+    bool atexit_set = false;
+    // no destructor: a function-static's destructor runs in an order unspecified relative
+    // to the HIP and RCCL runtimes' own teardown; rt_scene_shutdown (atexit) releases
+    void release() {
         if (ctx) rt_ctx_destroy(ctx);
         if (multi) rt_multi_destroy(multi);
+        ctx = nullptr;
+        multi = nullptr;
+        ctx_device = -1;
+        multi_devices.clear();
+        multi_transport = -1;
+        uploaded.clear();
     }
 };
 
 Global& global() {
-    static Global g;
-    return g;
+    static Global* g = new Global();  // never destroyed (see Global::release)
+    return *g;
+}
+
+/* After the first renderer exists (the HIP runtime — and RCCL for a tiled renderer — is
+ * initialised by then), so the handler runs before their exit-time teardown. */
+void register_shutdown(Global& g) {
+    if (g.atexit_set) return;
+    g.atexit_set = true;
+    std::atexit([] { rt_scene_shutdown(); });
 }
 
 void check(int st, rt_ctx* ctx, const char* what) {
@@ -60,6 +78,12 @@ void check_multi(int st, rt_multi* m, const char* what) {
 }
 
 }  // namespace
+
+void rt_scene_shutdown() {
+    Global& g = global();
+    std::lock_guard<std::mutex> lk(g.mu);
+    g.release();
+}
 
 void rt_scene_set_options(const RtSceneOptions& opts) {
     Global& g = global();
@@ -99,6 +123,7 @@ void rt_scene(std::vector<vec3> u, const std::vector<std::unique_ptr<SceneGeomet
         g.ctx_device = g.opts.device;
         g.uploaded.clear();
     }
+    register_shutdown(g);
     if (tiled != g.uploaded_tiled) g.uploaded.clear();
     g.uploaded_tiled = tiled;
     // the interactive loop renders the same scene frame after frame (main.cpp:329): keep it

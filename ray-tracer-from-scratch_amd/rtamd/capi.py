@@ -31,6 +31,7 @@ RT_ERR_COMM = 8
 
 RT_TRANSPORT_RCCL = 0
 RT_TRANSPORT_COPY = 1
+RT_TRANSPORT_RCCL_LOOPBACK = 2
 RT_MULTI_ID_BYTES = 128
 RT_MULTI_SLOTS = 2
 
@@ -133,6 +134,7 @@ SIGNATURES = [
     ("rt_band_rows", C.c_int,
      [C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     ("rt_max_depth", C.c_int32, []),
+    ("rt_tile_rows", C.c_int32, []),
     ("rt_frame_boxes", C.c_int,
      [C.POINTER(rt_prim), C.c_int32, C.POINTER(rt_camera), C.c_int32, C.c_int32,
       C.POINTER(C.c_int16), C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
@@ -258,9 +260,10 @@ def interleaved_rows(height: int, nparts: int, part: int) -> int:
 
 def interleaved_row_index(height: int, nparts: int, part: int):
     """Frame rows of interleaved part `part`, in the order the part stores them."""
+    th = load().rt_tile_rows()
     rows = []
-    for t in range(part, (height + 7) // 8, nparts):
-        rows.extend(range(8 * t, min(8 * t + 8, height)))
+    for t in range(part, (height + th - 1) // th, nparts):
+        rows.extend(range(th * t, min(th * t + th, height)))
     return rows
 
 

@@ -5,7 +5,10 @@ frame (pixels are independent; the reference renders the whole frame on one thre
 main.cpp:124-139).
 
 One GPU box has one device and RCCL takes one rank per GPU, so:
-  - RCCL is exercised at one rank (the communicator, the caller-stream protocol);
+  - RCCL runs at one rank through RT_TRANSPORT_RCCL_LOOPBACK: a communicator of one rank
+    and the root's band sent to itself (ncclCommInitRank, ncclGroupStart/End, ncclSend,
+    ncclRecv, ncclCommGetAsyncError all execute), bitwise against the one-GPU frame; the
+    plain RT_TRANSPORT_RCCL at one rank makes no communicator (nothing is exchanged);
   - the N-rank orchestration — band offsets, ragged and empty bands, double-buffered band
     slots, worker threads doing each rank's host work, caller-stream ordering — runs with
     N ranks on the same GPU through RT_TRANSPORT_COPY (peer copies instead of RCCL
@@ -35,12 +38,15 @@ def _cam(w, h, dx=0.0):
     return cam
 
 
-def test_single_rank_rccl_equals_render(rend):
-    """RCCL transport with one rank: the frame operator is rt_render of the whole frame."""
+@pytest.mark.parametrize("transport", [capi.RT_TRANSPORT_RCCL, capi.RT_TRANSPORT_RCCL_LOOPBACK])
+def test_single_rank_rccl_equals_render(rend, transport):
+    """One rank: the frame operator is rt_render of the whole frame — with the plain RCCL
+    transport (no communicator) and with the loopback transport, whose root renders into
+    its band slot and sends it to itself through a one-rank RCCL communicator."""
     sc = scenes.synthetic_scene(8, 4)
     prims = scenes.to_prims(sc)
     rend.set_scene(prims)
-    with capi.MultiRenderer([0]) as m:
+    with capi.MultiRenderer([0], transport=transport) as m:
         m.set_scene(prims)
         for (w, h) in ((160, 90), (1920, 1080)):
             cam = _cam(w, h)
@@ -85,7 +91,8 @@ def test_ragged_and_empty_bands(rend, n, w, h):
         assert np.array_equal(got.view(np.uint64), ref.view(np.uint64))
 
 
-@pytest.mark.parametrize("transport,n", [(capi.RT_TRANSPORT_COPY, 4), (capi.RT_TRANSPORT_RCCL, 1)])
+@pytest.mark.parametrize("transport,n", [(capi.RT_TRANSPORT_COPY, 4), (capi.RT_TRANSPORT_RCCL, 1),
+                                         (capi.RT_TRANSPORT_RCCL_LOOPBACK, 1)])
 def test_frames_in_flight_on_caller_streams(rend, transport, n):
     """The bench's frame loop: many frames of a moving camera enqueued back to back by one
     rt_multi_render_device_frames call into two device frame buffers on two caller streams
@@ -244,3 +251,59 @@ def test_multi_interleaved_layout_bitwise(rend, n):
                 assert np.array_equal(b.cpu().numpy().view(np.uint32), ref.view(np.uint32)), (n, w)
         with pytest.raises(capi.RTError):
             m.set_option(capi.RT_OPT_MULTI_LAYOUT, 2)
+
+
+def test_loopback_rccl_c4_full_size_and_interleaved_frames(rend):
+    """RT_TRANSPORT_RCCL_LOOPBACK at config 4's full size: PATH64 fp32 RGB, RGBA8 and F64
+    frames through RCCL send/recv (root to itself) bitwise the one-GPU frame, then 9 frames
+    in flight on two caller streams (the root's band slots reused while its self-sends are
+    pending), every frame complete on its stream; rt_multi_sync checks RCCL's async error."""
+    import torch
+    dev = torch.device("cuda", 0)
+    cfg = scenes.CONFIGS["c2"]
+    prims = scenes.to_prims(cfg.scene())
+    rend.set_scene(prims)
+    cam = _cam(cfg.width, cfg.height)
+    with capi.MultiRenderer([0], transport=capi.RT_TRANSPORT_RCCL_LOOPBACK) as m:
+        m.set_scene(prims)
+        for prec, fmt in ((capi.RT_PREC_PATH64, capi.RT_OUT_RGB_F32),
+                          (capi.RT_PREC_PATH64, capi.RT_OUT_RGBA8),
+                          (capi.RT_PREC_F64, capi.RT_OUT_RGB_F32)):
+            got, _ = m.render(cam, cfg.depth, prec, 0, fmt)
+            ref, _ = rend.render(cam, cfg.depth, prec, 0, fmt)
+            assert np.array_equal(got.view(np.uint8), ref.view(np.uint8)), (prec, fmt)
+        ref, _ = rend.render(cam, cfg.depth, capi.RT_PREC_PATH64, 0, capi.RT_OUT_RGB_F32)
+        bufs = [torch.full((cfg.height, cfg.width, 3), -1.0, device=dev) for _ in range(2)]
+        sts = [torch.cuda.Stream(dev) for _ in range(2)]
+        torch.cuda.synchronize()
+        m.render_device_frames([cam], cfg.depth, [b.data_ptr() for b in bufs], capi.RT_PREC_PATH64,
+                               streams=[s.cuda_stream for s in sts], nframes=9)
+        torch.cuda.synchronize()
+        m.sync()
+        for b in bufs:
+            assert np.array_equal(b.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+
+
+def test_failed_frame_breaks_the_communicator(rend):
+    """A frame that fails after the gather may have been queued (here: no scene on the
+    ranks yet) leaves the communicator out of step: the rt_multi reports RT_ERR_COMM on
+    every later frame and on rt_multi_sync (which aborts the communicator instead of
+    waiting), and destroying it returns (ncclCommAbort, no hang)."""
+    import torch
+    dev = torch.device("cuda", 0)
+    cam = _cam(64, 36)
+    buf = torch.zeros((36, 64, 3), device=dev)
+    m = capi.MultiRenderer([0], transport=capi.RT_TRANSPORT_RCCL_LOOPBACK)
+    try:
+        with pytest.raises(capi.RTError) as e1:
+            m.render_device(cam, 2, buf.data_ptr(), capi.RT_PREC_PATH64)
+        assert e1.value.status == capi.RT_ERR_NO_SCENE
+        m.set_scene(scenes.to_prims(scenes.synthetic_scene(8, 4)))
+        with pytest.raises(capi.RTError) as e2:
+            m.render_device(cam, 2, buf.data_ptr(), capi.RT_PREC_PATH64)
+        assert e2.value.status == capi.RT_ERR_COMM
+        with pytest.raises(capi.RTError) as e3:
+            m.sync()
+        assert e3.value.status == capi.RT_ERR_COMM
+    finally:
+        m.close()
