@@ -280,6 +280,45 @@ def main() -> int:
             H, W, ch, tdt, dev, depth=2)
         del band_bufs
 
+    # ---- the gathered frame against rank 0's own one-GPU render of the same frame, bitwise
+    # (untimed): the row-tiled operator must only move bytes (pixels are independent) ----
+    gather_check = None
+    if tiled_mode:
+        ref = None
+        nbytes = H * W * (4 if args.out == "rgba8" else 12)
+        if rank == 0:
+            ref = torch.empty((H, W, ch), dtype=tdt, device=dev)
+            rend.render_device(cam, depth, ref.data_ptr(), prec, flags, out_fmt,
+                               stream=stream.cuda_stream)
+        got = None
+        if multi is not None:
+            outs[0].fill_(-1.0)
+            torch.cuda.synchronize(dev)
+            multi.render_device_frames([cam], depth, out_ptrs[:1] if multi.has_root else [], prec,
+                                       flags, out_fmt, streams=st_ptrs[:1], nframes=1)
+            torch.cuda.synchronize(dev)
+            multi.sync()
+            if rank == 0:
+                got = outs[0].view(torch.uint8).flatten()[:nbytes]
+        elif torch_tiled is not None:
+            h_ = torch_tiled.submit()
+            torch_tiled.wait(h_)
+            torch_tiled.drain()
+            torch.cuda.synchronize(dev)
+            if rank == 0:
+                got = torch_tiled.frame(h_[0]).view(torch.uint8).flatten()[:nbytes]
+        barrier()
+        if rank == 0:
+            eq = bool(torch.equal(got, ref.view(torch.uint8).flatten()[:nbytes]))
+            gather_check = {"bitwise_equal_to_one_gpu_frame": eq, "ranks": world,
+                            "output": args.out,
+                            "operator": "rt_multi (RCCL send/recv)" if multi is not None
+                            else "rtamd.tiling (torch.distributed gather)"}
+            if not eq:
+                print(f"bench: the gathered {world}-rank frame differs from the one-GPU frame",
+                      file=sys.stderr)
+            del ref, got
+
     def run_steps(n: int):
         """n consecutive frames, enqueued by ONE C-ABI call (or the torch tiler's loop)."""
         if multi is not None:
@@ -664,6 +703,7 @@ def main() -> int:
             "frame_sharded": sharded,
             "tiled_rgba8": tiled8,
             "c5_tiled": c5,
+            "gather_check": gather_check,
         }
         if world == 1 and not args.no_cpu_baseline and args.cpu_seconds > 0:
             result["cpu_baseline"] = cpu_baseline(cfg, prims, cam0, depth, flags, args.cpu_seconds)

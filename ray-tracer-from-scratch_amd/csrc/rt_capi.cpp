@@ -93,7 +93,7 @@ struct rt_ctx {
     // waits for it — so its wave costs are not those of two frames sharing the CUs (frames
     // in flight overlap a frame's tail with the next one's start, which inflated or hid the
     // costs of the tiles dispatched first and could install a worse order for 32 frames)
-    bool fb_isolate = true;
+    bool fb_isolate = false;
     hipEvent_t ev_iso = nullptr;         // recorded behind the sampled frame
     bool iso_pending = false;
     std::vector<hipStream_t> iso_seen;   // streams already ordered behind ev_iso

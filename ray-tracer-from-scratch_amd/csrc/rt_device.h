@@ -106,7 +106,7 @@ constexpr int BIN_MAX_PRIMS = 64;
 // base-nW number w1..wL, off_L = nW + nW^2 + .. + nW^(L-1).
 constexpr int MIR_MAX_DEPTH = 3;
 #ifndef RT_MIR_MAX_BOXES
-#define RT_MIR_MAX_BOXES 1024
+#define RT_MIR_MAX_BOXES 256
 #endif
 constexpr int MIR_MAX_BOXES = RT_MIR_MAX_BOXES;
 struct PrimBox {

@@ -400,6 +400,31 @@ def test_path64_sun(rend, oracle):
     assert np.abs(img - o64).max() <= 4 * PATH64_TOL   # sun adds up to 1.64x colour
 
 
+def test_c2_sun_full_size(rend, oracle):
+    """Config 2's literal "+ sun" at full size (1920x1080, 8 spheres + 4 walls, depth 4,
+    RT_FLAG_SUN; the sun constants are main.cpp:18-19, unused by the reference, so the bar
+    is the oracle's sun): F64 + sun against the oracle on sampled row blocks (top, the
+    heavy middle, bottom) to 1e-12 with outliers only on discontinuities; PATH64 + sun
+    (the bench precision) against F64 + sun on every pixel, with the same segment count —
+    which is also the sun-off count (the sun adds shading terms, never rays)."""
+    cfg = scenes.CONFIGS["c2"]
+    sc = cfg.scene()
+    f64, s64, cam = render(rend, sc, cfg.width, cfg.height, cfg.depth, capi.RT_PREC_F64,
+                           flags=capi.RT_FLAG_SUN, fmt=capi.RT_OUT_RGB_F64, count_segments=True)
+    prims = scenes.to_prims(sc)
+    for r0 in (0, 536, 1072):
+        o64, _, _, sig = oracle.render(prims, cam, cfg.depth, flags=capi.RT_FLAG_SUN, row0=r0,
+                                       nrows=8, nthreads=NTHREADS, want_sig=True)
+        check_f64(f64[r0:r0 + 8], o64, sig, what=("c2 sun", r0))
+    p64, sp, _ = render(rend, sc, cfg.width, cfg.height, cfg.depth, capi.RT_PREC_PATH64,
+                        flags=capi.RT_FLAG_SUN, fmt=capi.RT_OUT_RGB_F32, count_segments=True)
+    _, s0, _ = render(rend, sc, cfg.width, cfg.height, cfg.depth, capi.RT_PREC_PATH64,
+                      fmt=capi.RT_OUT_RGB_F32, count_segments=True)
+    assert sp.segments == s64.segments == s0.segments
+    d = np.abs(p64 - f64)
+    assert np.isfinite(d).all() and d.max() <= 4 * PATH64_TOL, float(d.max())
+
+
 def test_non_integer_specular_exponent(rend, oracle):
     """A material with a non-integer exponent selects the general-pow kernel variants: OCML
     pow in fp64 (F64/MIXED: the reference's bar), the fp32 pow (`fpow`, exp2(e*log2 x)) in

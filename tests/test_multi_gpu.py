@@ -223,8 +223,8 @@ def test_interleaved_parts_bitwise(rend, scene, w, h, depth):
 def test_multi_interleaved_layout_bitwise(rend, n):
     """RT_OPT_MULTI_LAYOUT = 1 (interleaved tile rows): config 4's frame and a 256-sphere
     cull scene gathered from n ranks (peer copies, strided into the frame rows) are bitwise
-    the one-GPU frames, in one call and as frames in flight; switching layouts between
-    frames keeps them exact."""
+    the one-GPU frames, in one call and as frames in flight, fp32 RGB and the RGBA8
+    transport; switching layouts between frames keeps them exact."""
     import torch
     dev = torch.device("cuda", 0)
     cases = [(scenes.CONFIGS["c2"].scene(), 1920, 1080, 4),
@@ -240,6 +240,10 @@ def test_multi_interleaved_layout_bitwise(rend, n):
                 m.set_option(capi.RT_OPT_MULTI_LAYOUT, layout)
                 got, _ = m.render(cam, depth, capi.RT_PREC_PATH64)
                 assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), (n, w, layout)
+            # the RGBA8 transport (4 B/px parts, strided into the frame rows)
+            ref8, _ = rend.render(cam, depth, capi.RT_PREC_PATH64, 0, capi.RT_OUT_RGBA8)
+            got8, _ = m.render(cam, depth, capi.RT_PREC_PATH64, 0, capi.RT_OUT_RGBA8)
+            assert np.array_equal(got8, ref8), (n, w, "rgba8")
             bufs = [torch.full((h, w, 3), -1.0, device=dev) for _ in range(2)]
             sts = [torch.cuda.Stream(dev) for _ in range(2)]
             torch.cuda.synchronize()

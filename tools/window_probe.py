@@ -40,7 +40,8 @@ def main():
     outs = [torch.empty((cam.height, cam.width, 3), device=dev) for _ in range(args.fif)]
     ptrs = [o.data_ptr() for o in outs]
     segs = torch.zeros(1, dtype=torch.int64, device=dev)
-    for spec in args.variants.split(";"):
+    vars_ = []
+    for spec in args.variants.split(";"):   # every renderer first, warmed
         name, _, opts = spec.partition(":")
         r = capi.Renderer(0)
         r.set_option(capi.RT_OPT_BOX_CACHE, 0)
@@ -48,35 +49,40 @@ def main():
             k, v = kv.split("=")
             r.set_option(getattr(capi, "RT_OPT_" + k), int(v))
         r.set_scene(prims)
+        segs.zero_()
         r.render_device(cam, cfg.depth, ptrs[0], prec, d_segments=segs.data_ptr(), stream=sp[0])
         torch.cuda.synchronize()
         nseg = int(segs.item())
         r.render_device_frames([cam], cfg.depth, ptrs, prec, streams=sp, nframes=args.warm)
         torch.cuda.synchronize()
-        wall, gpu = [], []
-        for _ in range(args.windows):
+        vars_.append({"name": name, "opts": opts, "r": r, "nseg": nseg, "wall": [], "gpu": []})
+    # windows interleaved across the variants (drift of clocks/box cancels out)
+    for _ in range(args.windows):
+        for v in vars_:
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             t0 = time.perf_counter()
             e0.record(streams[0])
             for s in streams[1:]:
                 s.wait_stream(streams[0])
-            r.render_device_frames([cam], cfg.depth, ptrs, prec, streams=sp, nframes=args.steps)
+            v["r"].render_device_frames([cam], cfg.depth, ptrs, prec, streams=sp, nframes=args.steps)
             for s in streams[1:]:
                 streams[0].wait_stream(s)
             e1.record(streams[0])
             torch.cuda.synchronize()
-            wall.append((time.perf_counter() - t0) / args.steps * 1e3)
-            gpu.append(e0.elapsed_time(e1) / args.steps)
-        r.close()
+            v["wall"].append((time.perf_counter() - t0) / args.steps * 1e3)
+            v["gpu"].append(e0.elapsed_time(e1) / args.steps)
+    for v in vars_:
+        v["r"].close()
+        wall, gpu = v["wall"], v["gpu"]
         q = sorted(wall)
-        res = {"variant": name, "options": opts, "config": cfg.name, "precision": args.precision,
+        res = {"variant": v["name"], "options": v["opts"], "config": cfg.name, "precision": args.precision,
                "steps": args.steps, "fif": args.fif, "windows": args.windows,
                "wall_ms_median": round(statistics.median(wall), 4), "wall_ms_min": round(q[0], 4),
                "wall_ms_p90": round(q[int(0.9 * (len(q) - 1))], 4), "wall_ms_max": round(q[-1], 4),
                "gpu_ms_median": round(statistics.median(gpu), 4),
-               "grays_median": round(nseg / (statistics.median(wall) * 1e-3) / 1e9, 1),
-               "wall_ms": [round(v, 4) for v in wall]}
+               "grays_median": round(v["nseg"] / (statistics.median(wall) * 1e-3) / 1e9, 1),
+               "wall_ms": [round(x, 4) for x in wall]}
         print(json.dumps(res), flush=True)
 
 
