@@ -30,6 +30,9 @@
 #include "rt_device.h"
 #include <chrono>
 
+#ifndef RT_DRY_LAUNCH     // diagnostic build: 1 = no kernel launch in rt_render_device*,
+#define RT_DRY_LAUNCH 0   // 2 = nor rt_multi's per-frame runtime calls (never in the product)
+#endif
 #ifndef RT_HOST_PROFILE   // diagnostic build: per-phase host time of rt_render_device, printed
 #define RT_HOST_PROFILE 0 // to stderr by rt_ctx_destroy (never in the product)
 #endif
@@ -1453,8 +1456,11 @@ static int render_device_impl(rt_ctx* ctx, const rt_camera* cam, int32_t row0, i
     st = isolate_before(ctx, hs, sampled);
     if (st != RT_OK) return st;
     HP(2);
-    const int e = rt::launch_trace(p, precision, s, done);
+    // RT_DRY_LAUNCH (diagnostic builds, tools/multi_host_cost.py): every host step of the
+    // frame but the kernel launch, to separate the host's own work from the runtime's
+    const int e = RT_DRY_LAUNCH ? (int)hipSuccess : rt::launch_trace(p, precision, s, done);
     if (e != (int)hipSuccess) return hip_fail(ctx, (hipError_t)e, "launch k_trace");
+    if (RT_DRY_LAUNCH) return RT_OK;
     st = isolate_after(ctx, hs, sampled);
     if (st != RT_OK) return st;
     HP(3);

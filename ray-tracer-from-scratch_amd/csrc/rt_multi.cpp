@@ -164,6 +164,14 @@ struct SlowCall {
         hipError_t e_ = (call);                                \
         if (e_ != hipSuccess) return hip_err((m), e_, #call);  \
     } while (0)
+/* the per-frame runtime calls; a diagnostic build (RT_DRY_LAUNCH >= 2) skips them */
+#ifndef RT_DRY_LAUNCH
+#define RT_DRY_LAUNCH 0
+#endif
+#define MHIPF(m, call)                       \
+    do {                                     \
+        if (RT_DRY_LAUNCH < 2) MHIP(m, call); \
+    } while (0)
 #define MNCCL(m, call)                                           \
     do {                                                         \
         SlowCall sc_(#call);                                     \
@@ -263,11 +271,11 @@ int enqueue_rank(rt_multi* m, Rank* k, const Job& j) {
             // stream (once the slot's previous self-send has completed), sent to itself below
             st = ensure_bands(m, k, (size_t)max_part_rows(m, cam.height) * row_bytes);
             if (st != RT_OK) return st;
-            MHIP(m, hipStreamWaitEvent(j.stream, k->ev_sent[s], 0));
+            MHIPF(m, hipStreamWaitEvent(j.stream, k->ev_sent[s], 0));
             SlowCall sc_("rt_render_device (root, loopback)");
             st = render_part(m, k, j, pt, static_cast<char*>(k->band[s]), false, j.stream);
             if (st != RT_OK) return st;
-            MHIP(m, hipEventRecord(k->ev_rendered[s], j.stream));
+            MHIPF(m, hipEventRecord(k->ev_rendered[s], j.stream));
         } else if (nrows > 0) {
             // the root's rows, in place in the frame, on the caller's stream
             SlowCall sc_("rt_render_device (root)");
@@ -287,8 +295,8 @@ int enqueue_rank(rt_multi* m, Rank* k, const Job& j) {
                 for (auto& b : k->staging) MHIP(m, hipMalloc(&b, part_bytes * m->nranks));
                 k->staging_cap = part_bytes * m->nranks;
             }
-            MHIP(m, hipStreamWaitEvent(k->comm_stream, j.ev_in, 0));
-            if (lb) MHIP(m, hipStreamWaitEvent(k->comm_stream, k->ev_rendered[s], 0));
+            MHIPF(m, hipStreamWaitEvent(k->comm_stream, j.ev_in, 0));
+            if (lb) MHIPF(m, hipStreamWaitEvent(k->comm_stream, k->ev_rendered[s], 0));
             MNCCL(m, ncclGroupStart());
             if (lb) {
                 const size_t bytes = (size_t)nrows * row_bytes;
@@ -319,8 +327,8 @@ int enqueue_rank(rt_multi* m, Rank* k, const Job& j) {
                                       cam.height, g, row_bytes, k->comm_stream);
                     if (st != RT_OK) return st;
                 }
-            MHIP(m, hipEventRecord(k->ev_done, k->comm_stream));
-            if (lb) MHIP(m, hipEventRecord(k->ev_sent[s], k->comm_stream));  // slot s free again
+            MHIPF(m, hipEventRecord(k->ev_done, k->comm_stream));
+            if (lb) MHIPF(m, hipEventRecord(k->ev_sent[s], k->comm_stream));  // slot s free again
         }
         return RT_OK;
     }
@@ -329,31 +337,31 @@ int enqueue_rank(rt_multi* m, Rank* k, const Job& j) {
     st = ensure_bands(m, k, (size_t)max_part_rows(m, cam.height) * row_bytes);
     if (st != RT_OK) return st;
     // band buffer `s` is free once the send of frame k - RT_MULTI_SLOTS has completed
-    MHIP(m, hipStreamWaitEvent(k->render_stream[s], k->ev_sent[s], 0));
+    MHIPF(m, hipStreamWaitEvent(k->render_stream[s], k->ev_sent[s], 0));
     {
         SlowCall sc_("rt_render_device (band)");
         st = render_part(m, k, j, pt, static_cast<char*>(k->band[s]), false, k->render_stream[s]);
     }
     if (st != RT_OK) return st;
-    MHIP(m, hipEventRecord(k->ev_rendered[s], k->render_stream[s]));
-    MHIP(m, hipStreamWaitEvent(k->comm_stream, k->ev_rendered[s], 0));
+    MHIPF(m, hipEventRecord(k->ev_rendered[s], k->render_stream[s]));
+    MHIPF(m, hipStreamWaitEvent(k->comm_stream, k->ev_rendered[s], 0));
     if (m->rccl()) {
         MNCCL(m, ncclSend(k->band[s], bytes, ncclUint8, 0, k->comm, k->comm_stream));
     } else {
         // the root's rows may still be read by the caller's earlier work on the frame buffer
-        MHIP(m, hipStreamWaitEvent(k->comm_stream, j.ev_in, 0));
+        MHIPF(m, hipStreamWaitEvent(k->comm_stream, j.ev_in, 0));
         if (inter) {
             st = scatter_part(m, j.d_frame, static_cast<const char*>(k->band[s]), cam.height, k->rank,
                               row_bytes, k->comm_stream);
             if (st != RT_OK) return st;
         } else {
-            MHIP(m, hipMemcpyPeerAsync(j.d_frame + (size_t)pt.row0 * row_bytes, m->r[0]->device, k->band[s],
+            MHIPF(m, hipMemcpyPeerAsync(j.d_frame + (size_t)pt.row0 * row_bytes, m->r[0]->device, k->band[s],
                                        k->device, bytes, k->comm_stream));
         }
     }
-    MHIP(m, hipEventRecord(k->ev_sent[s], k->comm_stream));
+    MHIPF(m, hipEventRecord(k->ev_sent[s], k->comm_stream));
     if (j.stream && m->rccl() && !m->has_root())
-        MHIP(m, hipStreamWaitEvent(j.stream, k->ev_sent[s], 0));
+        MHIPF(m, hipStreamWaitEvent(j.stream, k->ev_sent[s], 0));
     return RT_OK;
 }
 
@@ -444,7 +452,7 @@ int render_frame(rt_multi* m, const rt_camera* cam, int32_t depth, int32_t preci
         j.ev_in = m->ev_in[slot];
         // one rank: the band is the frame, rendered in place in stream order; nothing else
         // writes the frame buffer, so no event is needed (it costs host time every frame)
-        if (m->nranks > 1 || m->gathers()) MHIP(m, hipEventRecord(j.ev_in, j.stream));
+        if (m->nranks > 1 || m->gathers()) MHIPF(m, hipEventRecord(j.ev_in, j.stream));
     } else {
         j.stream = static_cast<hipStream_t>(stream);
     }
@@ -478,9 +486,9 @@ int render_frame(rt_multi* m, const rt_camera* cam, int32_t depth, int32_t preci
         DevGuard dg(root->device);
         MHIP(m, dg.err);
         if (m->rccl()) {
-            MHIP(m, hipStreamWaitEvent(j.stream, root->ev_done, 0));
+            MHIPF(m, hipStreamWaitEvent(j.stream, root->ev_done, 0));
         } else {
-            for (int L = 1; L < m->nlocal; L++) MHIP(m, hipStreamWaitEvent(j.stream, m->r[L]->ev_sent[slot], 0));
+            for (int L = 1; L < m->nlocal; L++) MHIPF(m, hipStreamWaitEvent(j.stream, m->r[L]->ev_sent[slot], 0));
         }
     }
     return RT_OK;

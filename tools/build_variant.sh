@@ -9,6 +9,8 @@ F="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off -munsafe-fp-atom
 /opt/rocm/bin/hipcc $F "$@" -c csrc/rt_trace.hip -o "$B/rt_trace.o" &
 /opt/rocm/bin/hipcc $F "$@" -c csrc/rt_trace_stamp.hip -o "$B/rt_trace_stamp.o" &
 /opt/rocm/bin/hipcc $F "$@" -x hip -c csrc/rt_capi.cpp -o "$B/rt_capi.o" &
+/opt/rocm/bin/hipcc $F "$@" -x hip -c csrc/rt_multi.cpp -o "$B/rt_multi.o" &
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o "lib/ab/$name.so" "$B/rt_trace.o" "$B/rt_trace_stamp.o" "$B/rt_capi.o"
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o "lib/ab/$name.so" "$B/rt_trace.o" "$B/rt_trace_stamp.o" \
+    "$B/rt_capi.o" "$B/rt_multi.o" -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 echo "lib/ab/$name.so"
