@@ -148,6 +148,9 @@ __device__ unsigned long long g_diag[16];
 #ifndef RT_WPE_PATH64           // occupancy targets (waves_per_eu below), A/B knobs
 #define RT_WPE_PATH64 5
 #endif
+#ifndef RT_WPE_PATH64_CULL_BONUS  // PATH64 cull kernels, depth <= 8, no sun: 6 waves/SIMD (79
+#define RT_WPE_PATH64_CULL_BONUS 1   // VGPRs, no scratch; A/B c5 -4.1%, c3 -6.1% vs 5, round 4)
+#endif
 #ifndef RT_WPE_PATH64_LIN_BONUS
 #define RT_WPE_PATH64_LIN_BONUS 0
 #endif
@@ -2356,7 +2359,8 @@ constexpr int waves_per_eu() {
         // (5 waves: A/B c5 -7%, c3 -5% with 20 B of spills in the cull kernels; the sun
         // variants, whose spills would be 56-96 B, keep 4)
         w = RT_WPE_PATH64 - (tier == 2 ? 1 : 0) - (SUN ? 1 : 0) +
-            ((!CULL && !SUN && tier == 0) ? RT_WPE_PATH64_LIN_BONUS : 0);
+            ((!CULL && !SUN && tier == 0) ? RT_WPE_PATH64_LIN_BONUS : 0) +
+            ((CULL && !SUN && tier == 0) ? RT_WPE_PATH64_CULL_BONUS : 0);
     else
         w = (INT_EXP ? (SUN ? 3 : 4) : (SUN ? 2 : 3)) - (tier > 0 ? 1 : 0) -
             ((PREC == PREC_MIXED && CULL && MAXD >= 8) ? RT_WPE_MIXED_CULL_DROP : 0) +
