@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
-# Round-3 profiles (run on the GPU box via gpurun; every step has its own time limit):
+# Per-round profiles (ROUND=rNN) (run on the GPU box via gpurun; every step has its own time limit):
 #   1. rocprofv3 --kernel-trace --stats of the driver's bench command and of the one-stream
 #      bench (frames in flight 1: rocprof's average dispatch = bench kernel_ms)
 #   2. PMC passes, one counter group per pass, --kernel-trace only, on tools/kernel_runner.py:
@@ -9,7 +9,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-ROUND=${ROUND:-r03}; OUT=gpurun_out/prof_$ROUND
+ROUND=${ROUND:?set ROUND=rNN}; OUT=gpurun_out/prof_$ROUND
 CONFIGS=${CONFIGS:-c2 c1 c3 c5}; PRECS=${PRECS:-path64}
 mkdir -p "$OUT"
 if [ "${TRACES:-1}" = 1 ]; then
