@@ -59,8 +59,7 @@ struct rt_ctx {
         int nS = 0, nW = 0, nP = 0;
         bool int_exp = true;
         size_t off_s64 = 0, off_w32 = 0, off_w64 = 0, off_sj = 0, off_wj = 0, off_mat = 0,
-               off_mat32 = 0, off_wnn = 0, off_clu = 0, off_csph = 0, off_cord = 0, off_bord = 0,
-               total = 0;
+               off_mat32 = 0, off_wnn = 0, off_clu = 0, off_csph = 0, off_cord = 0, total = 0;
         int nclu = 0, clu_axis = 0;  // sphere clusters (rt_device.h), 0 = none
         float clu_oinf = 0.0f;
         std::vector<char> bytes;    // the device image of the scene (rt_device.h layout)
@@ -601,7 +600,6 @@ rt::KParams make_params(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, i
     p.clu = reinterpret_cast<const rt::Clu32*>(base + ctx->sc.off_clu);
     p.csph = reinterpret_cast<const rt::CluSph*>(base + ctx->sc.off_csph);
     p.cord = reinterpret_cast<const uint8_t*>(base + ctx->sc.off_cord);
-    p.bord = ctx->sc.off_bord ? reinterpret_cast<const uint16_t*>(base + ctx->sc.off_bord) : nullptr;
     p.nclu = ctx->sc.nclu;
     p.clu_axis = ctx->sc.clu_axis;
     p.clu_cos = ctx->clu_cos;
@@ -753,13 +751,6 @@ int pack_scene(const rt_prim* prims, int32_t n, rt_ctx::SceneHost& sc) {
     const size_t off_wnn = align_up(off_mat32 + (nS + nW) * sizeof(rt::DevMat32), 256);
     // sphere clusters (rt_device.h): leaves of <= CLU_SIZE spheres from median splits
     std::vector<std::vector<int>> leaves;
-    // the split tree over the leaves (inner nodes in creation order; child < 0 = leaf ~child)
-    struct Inner {
-        int child[2];
-        int axis;
-    };
-    std::vector<Inner> inner;
-    int root = 0;
     int clu_axis = 0;
     if (nS >= 2 * rt::CLU_SIZE && nS <= (size_t)rt::CLU_SIZE * rt::CLU_MAX) {
         std::vector<int> all(nS);
@@ -769,10 +760,10 @@ int pack_scene(const rt_prim* prims, int32_t n, rt_ctx::SceneHost& sc) {
             finite = finite && std::isfinite(a.c[0]) && std::isfinite(a.c[1]) &&
                      std::isfinite(a.c[2]) && std::isfinite(a.r);
         // median split on the widest axis of the centres until <= CLU_SIZE per leaf
-        std::function<int(std::vector<int>&, bool)> split = [&](std::vector<int>& ids, bool top) -> int {
+        std::function<void(std::vector<int>&, bool)> split = [&](std::vector<int>& ids, bool top) {
             if (ids.size() <= (size_t)rt::CLU_SIZE) {
                 leaves.push_back(ids);
-                return ~(int)(leaves.size() - 1);
+                return;
             }
             double lo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, hi[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
             for (int i : ids)
@@ -789,29 +780,18 @@ int pack_scene(const rt_prim* prims, int32_t n, rt_ctx::SceneHost& sc) {
                 return sph[a].c[ax] < sph[b].c[ax] || (sph[a].c[ax] == sph[b].c[ax] && a < b);
             });
             std::vector<int> l(ids.begin(), ids.begin() + mid), r(ids.begin() + mid, ids.end());
-            const int me = (int)inner.size();
-            inner.push_back(Inner{{0, 0}, ax});
-            const int cl = split(l, false);
-            const int cr = split(r, false);
-            inner[me].child[0] = cl;  // lower coordinates along axis
-            inner[me].child[1] = cr;
-            return me;
+            split(l, false);
+            split(r, false);
         };
-        if (finite) root = split(all, true);
-        if (leaves.size() > (size_t)rt::CLU_MAX) {
-            leaves.clear();
-            inner.clear();
-        }
+        if (finite) split(all, true);
+        if (leaves.size() > (size_t)rt::CLU_MAX) leaves.clear();
     }
     const size_t nclu = leaves.size();
-    // node records: the leaves 0 .. nclu-1, then the inner nodes (node nclu + k = inner[k])
-    const size_t nnode = nclu > 0 ? 2 * nclu - 1 : 0;
     const size_t off_clu = align_up(off_wnn + nW * 4 * sizeof(double), 256);
     // room for a multiple of four cluster records (the kernels read the boxes four at a time)
-    const size_t off_csph = align_up(off_clu + ((nnode + 3) & ~(size_t)3) * sizeof(rt::Clu32), 256);
+    const size_t off_csph = align_up(off_clu + ((nclu + 3) & ~(size_t)3) * sizeof(rt::Clu32), 256);
     const size_t off_cord = align_up(off_csph + nclu * rt::CLU_SIZE * sizeof(rt::CluSph), 256);
-    const size_t off_bord = align_up(off_cord + 8 * rt::CLU_MAX, 256);
-    const size_t total = align_up(off_bord + 8 * rt::BVH_ORD * sizeof(uint16_t), 256) + 256;
+    const size_t total = align_up(off_cord + 8 * rt::CLU_MAX, 256) + 256;
     sc.bytes.assign(total, 0);
     sc.total = total;
     std::vector<char>& host = sc.bytes;
@@ -882,46 +862,6 @@ int pack_scene(const rt_prim* prims, int32_t n, rt_ctx::SceneHost& sc) {
         for (int q = 0; q < 3; q++) {
             clu[c].lo[q] = (float)(lo[q] - m);
             clu[c].hi[q] = (float)(hi[q] + m);
-        }
-    }
-    // inner nodes: the union of their children's (already widened) boxes, so every ball
-    // below a node lies in its box with at least the leaves' margin
-    if (nclu > 1) {
-        std::function<void(int)> box_of = [&](int k) {
-            rt::Clu32& B = clu[nclu + k];
-            for (int q = 0; q < 3; q++) {
-                B.lo[q] = HUGE_VALF;
-                B.hi[q] = -HUGE_VALF;
-            }
-            for (int c : inner[k].child) {
-                if (c >= 0) box_of(c);
-                const rt::Clu32& C = c >= 0 ? clu[nclu + c] : clu[~c];
-                for (int q = 0; q < 3; q++) {
-                    B.lo[q] = std::min(B.lo[q], C.lo[q]);
-                    B.hi[q] = std::max(B.hi[q], C.hi[q]);
-                }
-            }
-        };
-        box_of(root);
-        // depth-first order per direction octant, the child nearer along the split axis
-        // first (octant bit a set = d_a < 0: the upper child is nearer); entry = node |
-        // skip << 7, skip = the position after the node's subtree
-        auto* bord = reinterpret_cast<uint16_t*>(host.data() + off_bord);
-        for (int o = 0; o < 8; o++) {
-            uint16_t* ord = bord + o * rt::BVH_ORD;
-            int pos = 0;
-            std::function<void(int)> dfs = [&](int c) {  // c >= 0 inner, < 0 leaf ~c
-                const int at = pos++;
-                const int node = c >= 0 ? (int)nclu + c : ~c;
-                if (c >= 0) {
-                    const int a = inner[c].axis;
-                    const bool flip = (o >> a) & 1;
-                    dfs(inner[c].child[flip ? 1 : 0]);
-                    dfs(inner[c].child[flip ? 0 : 1]);
-                }
-                ord[at] = (uint16_t)(node | (pos << 7));
-            };
-            dfs(root);
         }
     }
     for (size_t w = 0; w < nW; w++) {
@@ -998,7 +938,6 @@ int pack_scene(const rt_prim* prims, int32_t n, rt_ctx::SceneHost& sc) {
         }
     }
     sc.off_cord = off_cord;
-    sc.off_bord = nclu > 1 ? off_bord : 0;
     sc.off_wnn = off_wnn;
     sc.off_clu = off_clu;
     sc.off_csph = off_csph;

@@ -139,12 +139,6 @@ struct alignas(64) CluSph {
     int32_t pad[3];
 };
 static_assert(sizeof(Clu32) == 32 && sizeof(CluSph) == 64, "cluster layout");
-// The split tree over the leaves (the host's median splits): node records are Clu32 boxes,
-// leaves 0 .. nclu-1 then the inner nodes (each the union of its children's boxes).  Per
-// direction octant, a depth-first order with the child nearer along the node's split axis
-// first: entry = node | skip << 7, skip = the position after the node's subtree, so a lane
-// walks its octant's order with no stack (rt_trace.hip bvh_scan).  2*64-1 nodes fit 7 bits.
-constexpr int BVH_ORD = 128;
 
 // Dispatch order given explicitly: up to ROW_PERM_MAX units (tile rows of 8 pixel rows, or
 // parts of them), int16 each, in the kernel arguments.
@@ -200,7 +194,6 @@ struct KParams {
     const Clu32* clu;      // [nclu] sphere-cluster boxes (cull kernels), see above
     const CluSph* csph;    // [nclu * CLU_SIZE] their spheres in cluster order
     const uint8_t* cord;   // [8][CLU_MAX] cluster at each rank of each octant's order
-    const uint16_t* bord;  // [8][BVH_ORD] tree walk order per octant (null: no tree)
     int32_t nclu;          // 0 = no clusters
     int32_t clu_axis;      // axis of the first split (0..2): lanes walk clusters against it
     float clu_cos;         // wide-cone waves (cone cos(half-angle) < clu_cos) use clusters

@@ -1274,57 +1274,7 @@ __device__ __forceinline__ uint64_t clusters_mask(const KParams& p, const SlabRa
     }
     return (uint64_t)cm;
 }
-/* The wide-cone scan as a tree walk (RT_CLU_BVH): each lane walks its direction octant's
- * depth-first order of the split tree (rt_device.h BVH_ORD), near child first, entering a
- * node only when its box's entry distance does not exceed the lane's best hit — with the
- * clusters' margin, (1 - 1e-3) t |d| <= best, so a skipped subtree holds no ball the exact
- * test could accept at a distance < best — and stops at the order's end.  Lanes descend
- * on their own (a divergent loop over inner nodes) until each holds a leaf or is done, then
- * the wave tests the held leaves together, so a leaf's eight exact tests run once for all
- * the lanes that reached a leaf (while-while traversal).  The winner is order-independent
- * (sphere_exact<false>: a tie compares scene indices). */
-#ifndef RT_CLU_BVH
-#define RT_CLU_BVH 0
-#endif
-__device__ __forceinline__ void bvh_scan(const KParams& p, const RayD& r, bool alive, HitD& h) {
-    const f3 o = F3((float)r.o.x, (float)r.o.y, (float)r.o.z);
-    const f3 d = F3((float)r.d.x, (float)r.d.y, (float)r.d.z);
-    const SlabRay sr = slab_ray(o, d);
-    const bool near = fmax3abs(o.x, o.y, o.z) <= p.clu_oinf;
-    const uint16_t* ord = p.bord + clu_octant(d) * BVH_ORD;
-    const int nn = 2 * p.nclu - 1;  // positions 0 .. nn-1
-    int i = 0;
-    bool done = !alive;
-    while (__any(!done)) {
-        int leaf = -1;
-        while (!done && leaf < 0) {
-            DIAG(6);  // (diagnostic build) one node visit
-            const uint32_t e = ord[i];
-            const int node = (int)(e & 127u), skip = (int)(e >> 7);
-            const float t = near ? slab_t(p.clu[node], sr) : 0.0f;
-            const bool enter = (double)t * r.dlen * (1.0 - 1e-3) <= h.dist;
-            if (enter && node < p.nclu) leaf = node;
-            i = (enter && node >= p.nclu) ? i + 1 : skip;
-            if (leaf < 0 && i >= nn) done = true;
-        }
-        if (leaf >= 0) {
-            DIAG(14);  // (diagnostic build) one leaf tested
-            const CluSph* cs = p.csph + leaf * CLU_SIZE;
-#pragma unroll
-            for (int k = 0; k < CLU_SIZE; ++k) {
-                const int s = cs[k].slot;
-                if (s >= 0) sphere_exact<false>(cs[k].c, s, r, h, &p);
-            }
-            if (i >= nn) done = true;
-        }
-    }
-}
-
 __device__ __forceinline__ void clusters_scan(const KParams& p, const RayD& r, bool alive, HitD& h) {
-    if (RT_CLU_BVH && p.bord != nullptr) {
-        bvh_scan(p, r, alive, h);
-        return;
-    }
     const f3 o = F3((float)r.o.x, (float)r.o.y, (float)r.o.z);
     const f3 d = F3((float)r.d.x, (float)r.d.y, (float)r.d.z);
     const SlabRay sr = slab_ray(o, d);
