@@ -19,7 +19,29 @@ sys.path.insert(0, os.path.join(REPO, "ray-tracer-from-scratch_amd"))
 from rtamd import capi, scenes  # noqa: E402
 
 
-def interleaved_part(capi, torch, st, cam, depth, prec, prims, out, segs, N, r, n):
+def pipelined_us(torch, st, st2, launch_on, n, extra=()):
+    """Per-frame GPU time of n frames round-robin over 2 + len(extra) streams (frames in
+    flight: one frame's tail overlaps the next ones' start, as in bench.py's frame loop).
+    A first untimed pass warms every stream (its first launch carries one-time costs)."""
+    sts = [st, st2] + list(extra)
+    for timed in (False, True):
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for s_ in sts[1:]:
+            s_.wait_stream(st)
+        m = n if timed else len(sts)
+        for k in range(m):
+            launch_on(sts[k % len(sts)], k % 2)
+        for s_ in sts[1:]:
+            st.wait_stream(s_)
+        e1.record(st)
+        torch.cuda.synchronize()
+    return round(e0.elapsed_time(e1) / n * 1e3, 2)
+
+
+def interleaved_part(capi, torch, st, cam, depth, prec, prims, out, segs, N, r, n, st2=None, out2=None,
+                     extra=()):
     """One interleaved part's kernel / host time per frame and the bytes it sends."""
     W = cam.width
     nr = capi.interleaved_rows(cam.height, N, r)
@@ -29,6 +51,10 @@ def interleaved_part(capi, torch, st, cam, depth, prec, prims, out, segs, N, r, 
     def launch(d_seg=0):
         rend.render_device_interleaved(cam, depth, N, r, out.data_ptr(), prec,
                                        d_segments=d_seg, stream=st.cuda_stream)
+
+    def launch_on(s, b):
+        rend.render_device_interleaved(cam, depth, N, r, (out, out2)[b].data_ptr(), prec,
+                                       stream=s.cuda_stream)
     for _ in range(40):
         launch()
     segs.zero_()
@@ -45,8 +71,11 @@ def interleaved_part(capi, torch, st, cam, depth, prec, prims, out, segs, N, r, 
     e1.record(st)
     torch.cuda.synchronize()
     kms = e0.elapsed_time(e1) / n
+    fif2 = pipelined_us(torch, st, st2, launch_on, n)
+    fif4 = pipelined_us(torch, st, st2, launch_on, n, extra)
     rend.close()
-    return {"rank": r, "nrows": nr, "kernel_us": round(kms * 1e3, 2),
+    return {"rank": r, "nrows": nr, "kernel_us": round(kms * 1e3, 2), "kernel_us_fif2": fif2,
+            "kernel_us_fif4": fif4,
             "host_us": round(host_us, 2), "segments": int(segs.item()),
             "send_bytes_f32": 0 if r == 0 else nr * W * 12,
             "send_bytes_rgba8": 0 if r == 0 else nr * W * 4}
@@ -57,6 +86,7 @@ def main():
     ap.add_argument("--config", default="c2")
     ap.add_argument("--precision", default="path64")
     ap.add_argument("--launches", type=int, default=100)
+    ap.add_argument("--splits", default="1,2,4,8")
     ap.add_argument("--layout", choices=("contiguous", "interleaved"), default="contiguous")
     args = ap.parse_args()
     import torch
@@ -68,17 +98,20 @@ def main():
     H, W = cam.height, cam.width
     prec = capi.PRECISIONS[args.precision]
     out = torch.empty((H, W, 3), device=dev)
+    out2 = torch.empty((H, W, 3), device=dev)
+    st2 = torch.cuda.Stream(dev)
+    extra = [torch.cuda.Stream(dev) for _ in range(2)]   # 4 frames in flight
     segs = torch.zeros(1, dtype=torch.int64, device=dev)
     n = args.launches
     res = {"config": args.config, "precision": args.precision, "width": W, "height": H,
            "layout": args.layout, "splits": {}}
     inter = args.layout == "interleaved"
-    for N in (1, 2, 4, 8):
+    for N in [int(x) for x in args.splits.split(",")]:
         bands = []
         for r in range(N):
             if inter:
                 bands.append(interleaved_part(capi, torch, st, cam, cfg.depth, prec, prims, out,
-                                              segs, N, r, n))
+                                              segs, N, r, n, st2, out2, extra))
                 continue
             r0, nr = capi.band_rows(H, N, r)
             rend = capi.Renderer(0)
@@ -105,14 +138,21 @@ def main():
                                       streams=[st.cuda_stream], nframes=n)
             host_us = (time.perf_counter() - t0) / n * 1e6
             torch.cuda.synchronize()
+            lo = lambda s_, b: rend.render_device(cam, cfg.depth, (out, out2)[b].data_ptr(), prec,
+                                                  row0=r0, nrows=nr, stream=s_.cuda_stream)
+            fif2 = pipelined_us(torch, st, st2, lo, n)
+            fif4 = pipelined_us(torch, st, st2, lo, n, extra)
             rend.close()
             bands.append({"rank": r, "row0": r0, "nrows": nr, "kernel_us": round(kms * 1e3, 2),
+                          "kernel_us_fif2": fif2, "kernel_us_fif4": fif4,
                           "host_us": round(host_us, 2), "segments": int(segs.item()),
                           "send_bytes_f32": 0 if r == 0 else nr * W * 12,
                           "send_bytes_rgba8": 0 if r == 0 else nr * W * 4})
         res["splits"][N] = {
             "bands": bands,
             "max_kernel_us": max(b["kernel_us"] for b in bands),
+            "max_kernel_us_fif2": max(b["kernel_us_fif2"] for b in bands),
+            "max_kernel_us_fif4": max(b["kernel_us_fif4"] for b in bands),
             "max_host_us": max(b["host_us"] for b in bands),
             "root_in_bytes_f32": sum(b["send_bytes_f32"] for b in bands),
             "root_in_bytes_rgba8": sum(b["send_bytes_rgba8"] for b in bands),
