@@ -65,7 +65,9 @@ def main():
             e0.record(streams[0])
             for s in streams[1:]:
                 s.wait_stream(streams[0])
+            tc = time.perf_counter()
             v["r"].render_device_frames([cam], cfg.depth, ptrs, prec, streams=sp, nframes=args.steps)
+            v.setdefault("host", []).append((time.perf_counter() - tc) / args.steps * 1e3)
             for s in streams[1:]:
                 streams[0].wait_stream(s)
             e1.record(streams[0])
@@ -82,7 +84,9 @@ def main():
                "wall_ms_p90": round(q[int(0.9 * (len(q) - 1))], 4), "wall_ms_max": round(q[-1], 4),
                "gpu_ms_median": round(statistics.median(gpu), 4),
                "grays_median": round(v["nseg"] / (statistics.median(wall) * 1e-3) / 1e9, 1),
-               "wall_ms": [round(x, 4) for x in wall]}
+               "wall_ms": [round(x, 4) for x in wall],
+               "gpu_ms": [round(x, 4) for x in gpu],
+               "host_call_ms_per_frame": [round(x, 4) for x in v["host"]]}
         print(json.dumps(res), flush=True)
 
 
