@@ -8,6 +8,9 @@
 #ifndef RT_CLUSTER_COS_DEFAULT  // build-time default of RT_OPT_CLUSTER_COS (x 1000)
 #define RT_CLUSTER_COS_DEFAULT 400
 #endif
+#ifndef RT_CLU_SAH  // 1: sphere clusters from surface-area splits instead of median splits
+#define RT_CLU_SAH 0
+#endif
 #ifndef RT_WALL_ORDER_DEFAULT   // build-time default of RT_OPT_WALL_ORDER (A/B builds)
 #define RT_WALL_ORDER_DEFAULT 0
 #endif
@@ -774,8 +777,40 @@ int pack_scene(const rt_prim* prims, int32_t n, rt_ctx::SceneHost& sc) {
             int ax = 0;
             for (int q = 1; q < 3; q++)
                 if (hi[q] - lo[q] > hi[ax] - lo[ax]) ax = q;
+            size_t mid = ids.size() / 2;
+            if (RT_CLU_SAH) {
+                // surface-area split: over the three axes and the cut positions that keep the
+                // leaf count at its minimum (multiples of CLU_SIZE), the one minimising
+                // area(left box) * |left| + area(right box) * |right| (boxes of the balls)
+                const size_t n = ids.size();
+                double best = HUGE_VAL;
+                for (int q = 0; q < 3; q++) {
+                    std::vector<int> v(ids);
+                    std::sort(v.begin(), v.end(), [&](int a, int b) {
+                        return sph[a].c[q] < sph[b].c[q] || (sph[a].c[q] == sph[b].c[q] && a < b);
+                    });
+                    auto area = [&](size_t b0, size_t b1) {
+                        double l[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, h[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+                        for (size_t k = b0; k < b1; k++)
+                            for (int z = 0; z < 3; z++) {
+                                const double rr = std::fabs(sph[v[k]].r);
+                                l[z] = std::min(l[z], sph[v[k]].c[z] - rr);
+                                h[z] = std::max(h[z], sph[v[k]].c[z] + rr);
+                            }
+                        const double e0 = h[0] - l[0], e1 = h[1] - l[1], e2 = h[2] - l[2];
+                        return 2 * (e0 * e1 + e1 * e2 + e2 * e0);
+                    };
+                    for (size_t k = rt::CLU_SIZE; k < n; k += rt::CLU_SIZE) {
+                        const double c = area(0, k) * (double)k + area(k, n) * (double)(n - k);
+                        if (c < best) {
+                            best = c;
+                            ax = q;
+                            mid = k;
+                        }
+                    }
+                }
+            }
             if (top) clu_axis = ax;
-            const size_t mid = ids.size() / 2;
             std::nth_element(ids.begin(), ids.begin() + mid, ids.end(), [&](int a, int b) {
                 return sph[a].c[ax] < sph[b].c[ax] || (sph[a].c[ax] == sph[b].c[ax] && a < b);
             });

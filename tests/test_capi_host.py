@@ -127,6 +127,11 @@ def test_multi_args_rejected_without_device():
     assert lib.rt_multi_create(devs, 1, 2, 1, None, 0, C.byref(h)) == capi.RT_ERR_INVALID_ARG
     uid = (C.c_uint8 * capi.RT_MULTI_ID_BYTES)()
     assert lib.rt_multi_create(devs, 1, 2, 1, uid, 1, C.byref(h)) == capi.RT_ERR_UNSUPPORTED
+    # the loopback transport is an RCCL transport: one rank per GPU, the shared id across
+    # processes; an unknown transport is rejected
+    assert lib.rt_multi_create(devs, 1, 2, 1, None, capi.RT_TRANSPORT_RCCL_LOOPBACK,
+                               C.byref(h)) == capi.RT_ERR_INVALID_ARG
+    assert lib.rt_multi_create(devs, 1, 2, 0, None, 3, C.byref(h)) == capi.RT_ERR_INVALID_ARG
     if not has_gpu():
         assert lib.rt_multi_create(devs, 1, 1, 0, None, 0, C.byref(h)) == capi.RT_ERR_NO_DEVICE
     assert lib.rt_multi_destroy(None) == capi.RT_ERR_INVALID_ARG
@@ -139,6 +144,13 @@ def test_multi_args_rejected_without_device():
         capi.RT_ERR_INVALID_ARG
     assert lib.rt_multi_unique_id(None) == capi.RT_ERR_INVALID_ARG
     assert lib.rt_multi_last_error(None) == b""
+
+
+def test_tile_rows_is_the_interleaving_unit():
+    """rt_tile_rows(): the pixel rows per tile row of the kernels — the unit rt_multi's
+    interleaved layout deals and scatters (one constant for both)."""
+    assert capi.load().rt_tile_rows() == 8
+    assert capi.interleaved_row_index(17, 2, 1) == list(range(8, 16))
 
 
 def test_interleaved_rows_partition():
