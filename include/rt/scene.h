@@ -140,7 +140,8 @@ void rt_scene(std::vector<vec3> u, const std::vector<std::unique_ptr<SceneGeomet
  * depth (default 10) and flags (RT_FLAG_SUN).  `devices` with more than one entry renders
  * every frame row-tiled across those GPUs and gathers it into devices[0] (rt_multi_*,
  * BASELINE config 4; `transport` RT_TRANSPORT_RCCL, or RT_TRANSPORT_COPY, which also takes
- * one GPU listed several times); the frame is bitwise the one-GPU frame. */
+ * one GPU listed several times); one entry with RT_TRANSPORT_RCCL_LOOPBACK goes through
+ * the same operator with a one-rank communicator.  The frame is bitwise the one-GPU frame. */
 struct RtSceneOptions {
     int device = 0;
     int precision = RT_PREC_MIXED;

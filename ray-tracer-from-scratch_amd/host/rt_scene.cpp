@@ -104,7 +104,9 @@ void rt_scene(std::vector<vec3> u, const std::vector<std::unique_ptr<SceneGeomet
     // flatten first: a primitive the GPU path does not know throws before any device work
     std::vector<rt_prim> prims(scene.size());
     for (size_t j = 0; j < scene.size(); j++) scene[j]->pack(&prims[j]);
-    const bool tiled = g.opts.devices.size() > 1;
+    // several devices, or one with the loopback transport (the gather's RCCL calls on one GPU)
+    const bool tiled = g.opts.devices.size() > 1 ||
+                       (g.opts.devices.size() == 1 && g.opts.transport == RT_TRANSPORT_RCCL_LOOPBACK);
     if (tiled && (!g.multi || g.multi_devices != g.opts.devices ||
                   g.multi_transport != g.opts.transport)) {
         if (g.multi) rt_multi_destroy(g.multi);

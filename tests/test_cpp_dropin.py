@@ -64,11 +64,13 @@ def test_reference_style_plugin_compiles_and_is_reported(dropin):
 
 @pytest.mark.gpu
 @pytest.mark.skipif(not has_gpu(), reason="needs a HIP device")
-@pytest.mark.parametrize("n,transport", [(1, 0), (3, 1), (8, 1)])
+@pytest.mark.parametrize("n,transport", [(1, 0), (1, 2), (3, 1), (8, 1)])
 def test_rt_scene_row_tiled_over_devices(dropin, golden_frames, n, transport):
     """RtSceneOptions::devices: the C++ drop-in renders every frame row-tiled over the listed
-    ranks (rt_multi; RCCL for one rank, peer copies for several ranks on this box's one GPU)
-    — the reference's own depth-10 frame within 1e-12, bitwise the one-GPU drop-in."""
+    ranks (rt_multi: one device with RCCL is the plain one-GPU renderer; with the loopback
+    transport the frame goes through a one-rank RCCL communicator, released by the atexit
+    shutdown at process exit; peer copies for several ranks on this box's one GPU) — the
+    reference's own depth-10 frame within 1e-12, bitwise the one-GPU drop-in."""
     raw = subprocess.run([dropin, "render_multi", "48", "48", str(n), str(transport)],
                          capture_output=True, check=True).stdout
     img = np.frombuffer(raw, dtype=np.float64).reshape(48, 48, 3)
