@@ -71,8 +71,13 @@ def test_rt_scene_row_tiled_over_devices(dropin, golden_frames, n, transport):
     transport the frame goes through a one-rank RCCL communicator, released by the atexit
     shutdown at process exit; peer copies for several ranks on this box's one GPU) — the
     reference's own depth-10 frame within 1e-12, bitwise the one-GPU drop-in."""
-    raw = subprocess.run([dropin, "render_multi", "48", "48", str(n), str(transport)],
+    out = subprocess.run([dropin, "render_multi", "48", "48", str(n), str(transport)],
                          capture_output=True, check=True).stdout
+    # RCCL prints its version banner on stdout when a communicator is made (loopback):
+    # the frame is the last 48 x 48 x 3 doubles, after text lines only
+    nbytes = 48 * 48 * 3 * 8
+    raw, banner = out[-nbytes:], out[:-nbytes]
+    assert all(ln.isascii() for ln in banner.splitlines()), banner[:200]
     img = np.frombuffer(raw, dtype=np.float64).reshape(48, 48, 3)
     assert np.abs(img - golden_frames["default__48x48__d10"]).max() <= 1e-12
     one = subprocess.run([dropin, "render", "48", "48"], capture_output=True, check=True).stdout
