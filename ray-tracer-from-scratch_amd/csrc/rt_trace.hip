@@ -596,6 +596,34 @@ __device__ __forceinline__ float wsum(float v) {
     v += dpp<0x140>(v);
     return (lane_f(v, 0) + lane_f(v, 16)) + (lane_f(v, 32) + lane_f(v, 48));
 }
+#ifndef RT_DPP_ASM
+#define RT_DPP_ASM 1
+#endif
+#if RT_DPP_ASM
+/* In IEEE mode fminf/fmaxf of a value the compiler cannot prove canonical (a DPP move,
+ * a readlane) gets a v_max x,x,x canonicalise first, which also blocks folding the DPP
+ * move into the min: five VALU per step.  The operands here are never NaN (origins,
+ * cosines), so the steps are written as fused v_min/v_max_f32_dpp, one VALU each; the
+ * four row results meet through row_bcast:15 / row_bcast:31 in lane 63.  s_nop 1 before
+ * each DPP read covers the VALU-write -> DPP-read hazard the compiler cannot see. */
+#define RT_WRED(OP)                                                                        \
+    "s_nop 1\n\t" OP " %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"      \
+    "s_nop 1\n\t" OP " %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"      \
+    "s_nop 1\n\t" OP " %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"          \
+    "s_nop 1\n\t" OP " %0, %0, %0 row_mirror row_mask:0xf bank_mask:0xf\n\t"               \
+    "s_nop 1\n\t" OP " %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"             \
+    "s_nop 1\n\t" OP " %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"             \
+    "s_nop 1"
+__device__ __forceinline__ float wmin(float v) {
+    asm volatile(RT_WRED("v_min_f32_dpp") : "+v"(v));
+    return lane_f(v, 63);
+}
+__device__ __forceinline__ float wmax(float v) {
+    asm volatile(RT_WRED("v_max_f32_dpp") : "+v"(v));
+    return lane_f(v, 63);
+}
+#undef RT_WRED
+#else
 __device__ __forceinline__ float wmin(float v) {
     v = fminf(v, dpp<0xB1>(v));
     v = fminf(v, dpp<0x4E>(v));
@@ -610,6 +638,7 @@ __device__ __forceinline__ float wmax(float v) {
     v = fmaxf(v, dpp<0x140>(v));
     return fmaxf(fmaxf(lane_f(v, 0), lane_f(v, 16)), fmaxf(lane_f(v, 32), lane_f(v, 48)));
 }
+#endif
 __device__ __forceinline__ float uni(float v) { return v; }  // reductions are already scalar
 __device__ __forceinline__ double lane_d(double v, int l) {
     const long long b = __double_as_longlong(v);
