@@ -62,9 +62,12 @@ struct rt_ctx {
         int nS = 0, nW = 0, nP = 0;
         bool int_exp = true;
         size_t off_s64 = 0, off_w32 = 0, off_w64 = 0, off_sj = 0, off_wj = 0, off_mat = 0,
-               off_mat32 = 0, off_wnn = 0, off_clu = 0, off_csph = 0, off_cord = 0, total = 0;
-        int nclu = 0, clu_axis = 0;  // sphere clusters (rt_device.h), 0 = none
-        float clu_oinf = 0.0f;
+               off_mat32 = 0, off_wnn = 0, total = 0;
+        struct CluSet {  // sphere clusters (rt_device.h) of one leaf size, nclu 0 = none
+            size_t off_clu = 0, off_csph = 0, off_cord = 0;
+            int nclu = 0, clu_axis = 0, ls = 0;
+            float clu_oinf = 0.0f;
+        } cset[2];  // [0]: the F32 kernels' (CLU_SIZE), [1]: the fp64 kernels' (CLU_SIZE_D)
         std::vector<char> bytes;    // the device image of the scene (rt_device.h layout)
         std::vector<double> h_sph;  // nS x {cx, cy, cz, radius^2, radius}
         std::vector<double> h_wal;  // nW x {P, n, X, Y, length, width}
@@ -588,7 +591,7 @@ void frame_boxes(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t 
 
 rt::KParams make_params(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nrows,
                         int32_t depth, uint32_t flags, int32_t out_format, void* d_out,
-                        unsigned long long* d_segs) {
+                        unsigned long long* d_segs, int32_t precision) {
     rt::KParams p{};
     const char* base = static_cast<const char*>(ctx->d_scene);
     p.s32 = reinterpret_cast<const rt::SphG32*>(base);
@@ -600,13 +603,15 @@ rt::KParams make_params(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, i
     p.mat = reinterpret_cast<const rt::DevMat*>(base + ctx->sc.off_mat);
     p.mat32 = reinterpret_cast<const rt::DevMat32*>(base + ctx->sc.off_mat32);
     p.wnn = reinterpret_cast<const double(*)[4]>(base + ctx->sc.off_wnn);
-    p.clu = reinterpret_cast<const rt::Clu32*>(base + ctx->sc.off_clu);
-    p.csph = reinterpret_cast<const rt::CluSph*>(base + ctx->sc.off_csph);
-    p.cord = reinterpret_cast<const uint8_t*>(base + ctx->sc.off_cord);
-    p.nclu = ctx->sc.nclu;
-    p.clu_axis = ctx->sc.clu_axis;
+    const auto& cs = ctx->sc.cset[precision == RT_PREC_F32 ? 0 : 1];
+    p.clu = reinterpret_cast<const rt::Clu32*>(base + cs.off_clu);
+    p.csph = reinterpret_cast<const rt::CluSph*>(base + cs.off_csph);
+    p.cord = reinterpret_cast<const uint8_t*>(base + cs.off_cord);
+    p.nclu = cs.nclu;
+    p.clu_ls = cs.ls;
+    p.clu_axis = cs.clu_axis;
     p.clu_cos = ctx->clu_cos;
-    p.clu_oinf = ctx->sc.clu_oinf;
+    p.clu_oinf = cs.clu_oinf;
     p.nS = ctx->sc.nS;
     p.nW = ctx->sc.nW;
     p.int_exp = ctx->sc.int_exp ? 1 : 0;
@@ -752,82 +757,101 @@ int pack_scene(const rt_prim* prims, int32_t n, rt_ctx::SceneHost& sc) {
     const size_t off_mat = align_up(off_wj + nW * sizeof(int32_t), 256);
     const size_t off_mat32 = align_up(off_mat + (nS + nW) * sizeof(rt::DevMat), 256);
     const size_t off_wnn = align_up(off_mat32 + (nS + nW) * sizeof(rt::DevMat32), 256);
-    // sphere clusters (rt_device.h): leaves of <= CLU_SIZE spheres from binary splits (the
-    // surface-area cut at a multiple of CLU_SIZE, RT_CLU_SAH; else the median of the widest axis)
-    std::vector<std::vector<int>> leaves;
-    int clu_axis = 0;
-    if (nS >= 2 * rt::CLU_SIZE && nS <= (size_t)rt::CLU_SIZE * rt::CLU_MAX) {
-        std::vector<int> all(nS);
-        for (size_t s = 0; s < nS; s++) all[s] = (int)s;
-        bool finite = true;
-        for (const Sph& a : sph)
-            finite = finite && std::isfinite(a.c[0]) && std::isfinite(a.c[1]) &&
-                     std::isfinite(a.c[2]) && std::isfinite(a.r);
-        // median split on the widest axis of the centres until <= CLU_SIZE per leaf
-        std::function<void(std::vector<int>&, bool)> split = [&](std::vector<int>& ids, bool top) {
-            if (ids.size() <= (size_t)rt::CLU_SIZE) {
-                leaves.push_back(ids);
-                return;
-            }
-            double lo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, hi[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
-            for (int i : ids)
-                for (int q = 0; q < 3; q++) {
-                    lo[q] = std::min(lo[q], sph[i].c[q]);
-                    hi[q] = std::max(hi[q], sph[i].c[q]);
+    auto make_leaves = [&](int ls, std::vector<std::vector<int>>& leaves, int& clu_axis) {
+        // sphere clusters (rt_device.h): leaves of <= ls spheres from binary splits (the
+        // surface-area cut at a multiple of ls, RT_CLU_SAH; else the median of the widest axis)
+        if (nS >= 2 * (size_t)ls && nS <= (size_t)ls * rt::CLU_MAX) {
+            std::vector<int> all(nS);
+            for (size_t s = 0; s < nS; s++) all[s] = (int)s;
+            bool finite = true;
+            for (const Sph& a : sph)
+                finite = finite && std::isfinite(a.c[0]) && std::isfinite(a.c[1]) &&
+                         std::isfinite(a.c[2]) && std::isfinite(a.r);
+            // median split on the widest axis of the centres until <= ls per leaf
+            std::function<void(std::vector<int>&, bool)> split = [&](std::vector<int>& ids, bool top) {
+                if (ids.size() <= (size_t)ls) {
+                    leaves.push_back(ids);
+                    return;
                 }
-            int ax = 0;
-            for (int q = 1; q < 3; q++)
-                if (hi[q] - lo[q] > hi[ax] - lo[ax]) ax = q;
-            size_t mid = ids.size() / 2;
-            if (RT_CLU_SAH) {
-                // surface-area split: over the three axes and the cut positions that keep the
-                // leaf count at its minimum (multiples of CLU_SIZE), the one minimising
-                // area(left box) * |left| + area(right box) * |right| (boxes of the balls)
-                const size_t n = ids.size();
-                double best = HUGE_VAL;
-                for (int q = 0; q < 3; q++) {
-                    std::vector<int> v(ids);
-                    std::sort(v.begin(), v.end(), [&](int a, int b) {
-                        return sph[a].c[q] < sph[b].c[q] || (sph[a].c[q] == sph[b].c[q] && a < b);
-                    });
-                    auto area = [&](size_t b0, size_t b1) {
-                        double l[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, h[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
-                        for (size_t k = b0; k < b1; k++)
-                            for (int z = 0; z < 3; z++) {
-                                const double rr = std::fabs(sph[v[k]].r);
-                                l[z] = std::min(l[z], sph[v[k]].c[z] - rr);
-                                h[z] = std::max(h[z], sph[v[k]].c[z] + rr);
+                double lo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, hi[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+                for (int i : ids)
+                    for (int q = 0; q < 3; q++) {
+                        lo[q] = std::min(lo[q], sph[i].c[q]);
+                        hi[q] = std::max(hi[q], sph[i].c[q]);
+                    }
+                int ax = 0;
+                for (int q = 1; q < 3; q++)
+                    if (hi[q] - lo[q] > hi[ax] - lo[ax]) ax = q;
+                size_t mid = ids.size() / 2;
+                if (RT_CLU_SAH) {
+                    // surface-area split: over the three axes and the cut positions that keep the
+                    // leaf count at its minimum (multiples of CLU_SIZE), the one minimising
+                    // area(left box) * |left| + area(right box) * |right| (boxes of the balls)
+                    const size_t n = ids.size();
+                    double best = HUGE_VAL;
+                    for (int q = 0; q < 3; q++) {
+                        std::vector<int> v(ids);
+                        std::sort(v.begin(), v.end(), [&](int a, int b) {
+                            return sph[a].c[q] < sph[b].c[q] || (sph[a].c[q] == sph[b].c[q] && a < b);
+                        });
+                        auto area = [&](size_t b0, size_t b1) {
+                            double l[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, h[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+                            for (size_t k = b0; k < b1; k++)
+                                for (int z = 0; z < 3; z++) {
+                                    const double rr = std::fabs(sph[v[k]].r);
+                                    l[z] = std::min(l[z], sph[v[k]].c[z] - rr);
+                                    h[z] = std::max(h[z], sph[v[k]].c[z] + rr);
+                                }
+                            const double e0 = h[0] - l[0], e1 = h[1] - l[1], e2 = h[2] - l[2];
+                            return 2 * (e0 * e1 + e1 * e2 + e2 * e0);
+                        };
+                        for (size_t k = (size_t)ls; k < n; k += (size_t)ls) {
+                            const double c = area(0, k) * (double)k + area(k, n) * (double)(n - k);
+                            if (c < best) {
+                                best = c;
+                                ax = q;
+                                mid = k;
                             }
-                        const double e0 = h[0] - l[0], e1 = h[1] - l[1], e2 = h[2] - l[2];
-                        return 2 * (e0 * e1 + e1 * e2 + e2 * e0);
-                    };
-                    for (size_t k = rt::CLU_SIZE; k < n; k += rt::CLU_SIZE) {
-                        const double c = area(0, k) * (double)k + area(k, n) * (double)(n - k);
-                        if (c < best) {
-                            best = c;
-                            ax = q;
-                            mid = k;
                         }
                     }
                 }
-            }
-            if (top) clu_axis = ax;
-            std::nth_element(ids.begin(), ids.begin() + mid, ids.end(), [&](int a, int b) {
-                return sph[a].c[ax] < sph[b].c[ax] || (sph[a].c[ax] == sph[b].c[ax] && a < b);
-            });
-            std::vector<int> l(ids.begin(), ids.begin() + mid), r(ids.begin() + mid, ids.end());
-            split(l, false);
-            split(r, false);
-        };
-        if (finite) split(all, true);
-        if (leaves.size() > (size_t)rt::CLU_MAX) leaves.clear();
+                if (top) clu_axis = ax;
+                std::nth_element(ids.begin(), ids.begin() + mid, ids.end(), [&](int a, int b) {
+                    return sph[a].c[ax] < sph[b].c[ax] || (sph[a].c[ax] == sph[b].c[ax] && a < b);
+                });
+                std::vector<int> l(ids.begin(), ids.begin() + mid), r(ids.begin() + mid, ids.end());
+                split(l, false);
+                split(r, false);
+            };
+            if (finite) split(all, true);
+            if (leaves.size() > (size_t)rt::CLU_MAX) leaves.clear();
+        }
+    };
+    // set 0: the F32 kernels' leaves (CLU_SIZE); set 1: the fp64 kernels' (CLU_SIZE_D, or
+    // CLU_SIZE when that needs more than CLU_MAX leaves)
+    std::vector<std::vector<int>> leaves[2];
+    int clu_axis[2] = {0, 0}, lsz[2] = {rt::CLU_SIZE, rt::CLU_SIZE_D};
+    make_leaves(lsz[0], leaves[0], clu_axis[0]);
+    make_leaves(lsz[1], leaves[1], clu_axis[1]);
+    if (leaves[1].empty() && lsz[1] != lsz[0]) {
+        leaves[1] = leaves[0];
+        clu_axis[1] = clu_axis[0];
+        lsz[1] = lsz[0];
     }
-    const size_t nclu = leaves.size();
-    const size_t off_clu = align_up(off_wnn + nW * 4 * sizeof(double), 256);
-    // room for a multiple of four cluster records (the kernels read the boxes four at a time)
-    const size_t off_csph = align_up(off_clu + ((nclu + 3) & ~(size_t)3) * sizeof(rt::Clu32), 256);
-    const size_t off_cord = align_up(off_csph + nclu * rt::CLU_SIZE * sizeof(rt::CluSph), 256);
-    const size_t total = align_up(off_cord + 8 * rt::CLU_MAX, 256) + 256;
+    size_t off = align_up(off_wnn + nW * 4 * sizeof(double), 256);
+    for (int q = 0; q < 2; q++) {
+        auto& cs = sc.cset[q];
+        const size_t nclu = leaves[q].size();
+        cs.nclu = (int)nclu;
+        cs.clu_axis = clu_axis[q];
+        cs.ls = lsz[q];
+        cs.off_clu = off;
+        // room for a multiple of four cluster records (the kernels read the boxes in batches)
+        cs.off_csph = align_up(cs.off_clu + ((nclu + 3) & ~(size_t)3) * sizeof(rt::Clu32), 256);
+        cs.off_cord = align_up(cs.off_csph + nclu * lsz[q] * sizeof(rt::CluSph), 256);
+        off = align_up(cs.off_cord + 8 * rt::CLU_MAX, 256);
+    }
+    const size_t total = off + 256;
     sc.bytes.assign(total, 0);
     sc.total = total;
     std::vector<char>& host = sc.bytes;
@@ -840,8 +864,6 @@ int pack_scene(const rt_prim* prims, int32_t n, rt_ctx::SceneHost& sc) {
     auto* mat = reinterpret_cast<rt::DevMat*>(host.data() + off_mat);
     auto* mat32 = reinterpret_cast<rt::DevMat32*>(host.data() + off_mat32);
     auto* wnn = reinterpret_cast<double(*)[4]>(host.data() + off_wnn);
-    auto* clu = reinterpret_cast<rt::Clu32*>(host.data() + off_clu);
-    auto* csph = reinterpret_cast<rt::CluSph*>(host.data() + off_csph);
     auto put_mat = [&](size_t slot, const rt_material& m) {
         rt::DevMat& d = mat[slot];
         for (int k = 0; k < 3; k++) d.color[k] = m.color[k];
@@ -870,35 +892,61 @@ int pack_scene(const rt_prim* prims, int32_t n, rt_ctx::SceneHost& sc) {
         sj[s] = sph[s].j;
         put_mat(s, prims[sph[s].j].mat);
     }
-    double clu_scale = 1.0;
-    std::vector<std::array<double, 3>> cen(nclu);
-    for (size_t c = 0; c < nclu; c++) {
-        double lo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, hi[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
-        double scale = 1.0;
-        for (size_t k = 0; k < (size_t)rt::CLU_SIZE; k++) {
-            rt::CluSph& cs = csph[c * rt::CLU_SIZE + k];
-            cs.slot = -1;
-            if (k >= leaves[c].size()) continue;
-            const int si = leaves[c][k];
-            for (int q = 0; q < 4; q++) cs.c[q] = s64[si / 4].v[si % 4][q];
-            for (int q = 0; q < 4; q++) cs.f[q] = s32[si / 4].c[q][si % 4];
-            cs.slot = si;
+    for (int set = 0; set < 2; set++) {
+        auto& cset = sc.cset[set];
+        const size_t nclu = (size_t)cset.nclu, ls = (size_t)cset.ls;
+        const std::vector<std::vector<int>>& lv = leaves[set];
+        auto* clu = reinterpret_cast<rt::Clu32*>(host.data() + cset.off_clu);
+        auto* csph = reinterpret_cast<rt::CluSph*>(host.data() + cset.off_csph);
+        double clu_scale = 1.0;
+        std::vector<std::array<double, 3>> cen(nclu);
+        for (size_t c = 0; c < nclu; c++) {
+            double lo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, hi[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+            double scale = 1.0;
+            for (size_t k = 0; k < ls; k++) {
+                rt::CluSph& cs = csph[c * ls + k];
+                cs.slot = -1;
+                if (k >= lv[c].size()) continue;
+                const int si = lv[c][k];
+                for (int q = 0; q < 4; q++) cs.c[q] = s64[si / 4].v[si % 4][q];
+                for (int q = 0; q < 4; q++) cs.f[q] = s32[si / 4].c[q][si % 4];
+                cs.slot = si;
+                for (int q = 0; q < 3; q++) {
+                    const double rr = std::fabs(sph[si].r);
+                    lo[q] = std::min(lo[q], sph[si].c[q] - rr);
+                    hi[q] = std::max(hi[q], sph[si].c[q] + rr);
+                    scale = std::max(scale, std::fabs(sph[si].c[q]) + rr);
+                }
+            }
+            // margin: far above the fp32 rounding of the box, the ray and the slab arithmetic
+            // (~1e-6 relative), so a ray the exact test finds hitting a ball enters the box
+            const double m = 1e-3 * scale;
+            clu_scale = std::max(clu_scale, scale);
+            for (int q = 0; q < 3; q++) cen[c][q] = 0.5 * (lo[q] + hi[q]);
             for (int q = 0; q < 3; q++) {
-                const double rr = std::fabs(sph[si].r);
-                lo[q] = std::min(lo[q], sph[si].c[q] - rr);
-                hi[q] = std::max(hi[q], sph[si].c[q] + rr);
-                scale = std::max(scale, std::fabs(sph[si].c[q]) + rr);
+                clu[c].lo[q] = (float)(lo[q] - m);
+                clu[c].hi[q] = (float)(hi[q] + m);
             }
         }
-        // margin: far above the fp32 rounding of the box, the ray and the slab arithmetic
-        // (~1e-6 relative), so a ray the exact test finds hitting a ball enters the box
-        const double m = 1e-3 * scale;
-        clu_scale = std::max(clu_scale, scale);
-        for (int q = 0; q < 3; q++) cen[c][q] = 0.5 * (lo[q] + hi[q]);
-        for (int q = 0; q < 3; q++) {
-            clu[c].lo[q] = (float)(lo[q] - m);
-            clu[c].hi[q] = (float)(hi[q] + m);
+        // near-to-far cluster order per direction octant: by the box centre along the octant's
+        // diagonal (any order is exact; this one lets the lanes' pruning start from near hits)
+        auto* cord = reinterpret_cast<uint8_t*>(host.data() + cset.off_cord);
+        for (int o = 0; o < 8 && nclu > 0; o++) {
+            const double sx = (o & 1) ? -1.0 : 1.0, sy = (o & 2) ? -1.0 : 1.0, sz = (o & 4) ? -1.0 : 1.0;
+            std::vector<int> ord(nclu);
+            for (size_t c = 0; c < nclu; c++) ord[c] = (int)c;
+            std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) {
+                return sx * cen[a][0] + sy * cen[a][1] + sz * cen[a][2] <
+                       sx * cen[b][0] + sy * cen[b][1] + sz * cen[b][2];
+            });
+            for (size_t k = 0; k < nclu; k++) {
+                cord[o * rt::CLU_MAX + k] = (uint8_t)ord[k];
+                clu[ord[k]].rank[o] = (uint8_t)k;
+            }
         }
+        // origins up to 100x the scene's extent: fp32 errors of the slab test ~1e-5 x scale,
+        // 100x below the box margin
+        cset.clu_oinf = (float)(100.0 * clu_scale);
     }
     for (size_t w = 0; w < nW; w++) {
         const Wal& a = wal[w];
@@ -957,31 +1005,7 @@ int pack_scene(const rt_prim* prims, int32_t n, rt_ctx::SceneHost& sc) {
     sc.off_wj = off_wj;
     sc.off_mat = off_mat;
     sc.off_mat32 = off_mat32;
-    // near-to-far cluster order per direction octant: by the box centre along the octant's
-    // diagonal (any order is exact; this one lets the lanes' pruning start from near hits)
-    auto* cord = reinterpret_cast<uint8_t*>(host.data() + off_cord);
-    for (int o = 0; o < 8 && nclu > 0; o++) {
-        const double sx = (o & 1) ? -1.0 : 1.0, sy = (o & 2) ? -1.0 : 1.0, sz = (o & 4) ? -1.0 : 1.0;
-        std::vector<int> ord(nclu);
-        for (size_t c = 0; c < nclu; c++) ord[c] = (int)c;
-        std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) {
-            return sx * cen[a][0] + sy * cen[a][1] + sz * cen[a][2] <
-                   sx * cen[b][0] + sy * cen[b][1] + sz * cen[b][2];
-        });
-        for (size_t k = 0; k < nclu; k++) {
-            cord[o * rt::CLU_MAX + k] = (uint8_t)ord[k];
-            clu[ord[k]].rank[o] = (uint8_t)k;
-        }
-    }
-    sc.off_cord = off_cord;
     sc.off_wnn = off_wnn;
-    sc.off_clu = off_clu;
-    sc.off_csph = off_csph;
-    sc.nclu = (int)nclu;
-    sc.clu_axis = clu_axis;
-    // origins up to 100x the scene's extent: fp32 errors of the slab test ~1e-5 x scale,
-    // 100x below the box margin
-    sc.clu_oinf = (float)(100.0 * clu_scale);
     return RT_OK;
 }
 
@@ -1164,7 +1188,8 @@ int rt_frame_boxes(const rt_prim* prims, int32_t n, const rt_camera* cam, int32_
     ctx->wave_cull_min = 0x7fffffff;  // as the linear-scan kernels see the scene
     std::unique_ptr<rt::KParams> p(new (std::nothrow) rt::KParams);
     if (!p) return RT_ERR_OUT_OF_MEMORY;
-    *p = make_params(ctx.get(), cam, row0, nrows, 0, 0, RT_OUT_RGB_F32, nullptr, nullptr);
+    *p = make_params(ctx.get(), cam, row0, nrows, 0, 0, RT_OUT_RGB_F32, nullptr, nullptr,
+                     RT_PREC_F64);
     long total = p->nbox;
     for (long L = 1, lvl = 1; L <= p->mir_depth; L++) {
         lvl *= ctx->sc.nW;
@@ -1467,7 +1492,7 @@ static int render_device_impl(rt_ctx* ctx, const rt_camera* cam, int32_t row0, i
     // an interleaved part's tile rows span the frame: its pixel boxes are the whole frame's
     rt::KParams p = make_params(ctx, cam, nparts > 1 ? 0 : row0, nparts > 1 ? cam->height : nrows,
                                 depth, flags, out_format, d_out,
-                                reinterpret_cast<unsigned long long*>(d_segments));
+                                reinterpret_cast<unsigned long long*>(d_segments), precision);
     if (nparts > 1) {
         p.row0 = 0;
         p.nrows = nrows;
@@ -1569,7 +1594,7 @@ int rt_render(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nrows, in
     unsigned long long* segs = count_segments ? ctx->d_segs : nullptr;
     if (segs) RT_HIP(ctx, hipMemsetAsync(segs, 0, sizeof *segs, ctx->stream));
     rt::KParams p = make_params(ctx, cam, row0, nrows, depth, flags, out_format,
-                                ctx->d_out, segs);
+                                ctx->d_out, segs, precision);
     st = prepare_rows(ctx, cam, row0, nrows, ctx->stream, p);
     if (st != RT_OK) return st;
     RT_HIP(ctx, hipEventRecord(ctx->ev0, ctx->stream));

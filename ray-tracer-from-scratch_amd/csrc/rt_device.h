@@ -121,11 +121,20 @@ struct PrimBox {
 // exact test on the spheres of its own leaves only: a wave's iteration count is its worst
 // lane's, not the union of its lanes' candidates (which is what the wave cone pays when the
 // live rays point everywhere).
+// Two leaf sizes, one cluster set each: the F32 kernels' walk (cheap sphere tests, so the
+// box pass dominates) wants few leaves, the fp64 kernels' walk (exact fp64 tests) small ones
+// (A/B round 4: leaves of 4 vs 8, c3 PATH64 -6%, c5 -0.5..0.9%, but F32 c5 +7.6%).  The fp64
+// set falls back to CLU_SIZE leaves when its own would exceed CLU_MAX.
 #ifndef RT_CLU_SIZE
 #define RT_CLU_SIZE 8
 #endif
-constexpr int CLU_SIZE = RT_CLU_SIZE;
+#ifndef RT_CLU_SIZE_D
+#define RT_CLU_SIZE_D 4
+#endif
+constexpr int CLU_SIZE = RT_CLU_SIZE;      // F32 kernels
+constexpr int CLU_SIZE_D = RT_CLU_SIZE_D;  // fp64-path kernels (F64, MIXED, PATH64)
 constexpr int CLU_MAX = 64;
+static_assert(CLU_SIZE_D <= CLU_SIZE, "the fp64 walk's loop covers CLU_SIZE_D or CLU_SIZE");
 struct alignas(32) Clu32 {
     float lo[3], hi[3];
     uint8_t rank[8];  // position of this cluster in the near-to-far order of each direction
@@ -192,9 +201,10 @@ struct KParams {
     double eye_s[EYE_MAX_S][4];         // sphere s: {oc.x, oc.y, oc.z, |oc|^2 - r^2}
     double eye_w[EYE_MAX_W];            // wall w: dot(P - pos, n)
     const Clu32* clu;      // [nclu] sphere-cluster boxes (cull kernels), see above
-    const CluSph* csph;    // [nclu * CLU_SIZE] their spheres in cluster order
+    const CluSph* csph;    // [nclu * clu_ls] their spheres in cluster order
     const uint8_t* cord;   // [8][CLU_MAX] cluster at each rank of each octant's order
     int32_t nclu;          // 0 = no clusters
+    int32_t clu_ls;        // spheres per leaf record: CLU_SIZE_D or CLU_SIZE (F32: CLU_SIZE)
     int32_t clu_axis;      // axis of the first split (0..2): lanes walk clusters against it
     float clu_cos;         // wide-cone waves (cone cos(half-angle) < clu_cos) use clusters
     float clu_oinf;        // rays whose |origin|inf exceeds it test every cluster (the box

@@ -1330,9 +1330,13 @@ __device__ __forceinline__ void clusters_scan(const KParams& p, const RayD& r, b
             const float t = near ? slab_t(p.clu[c], sr) : 0.0f;
             if ((double)t * r.dlen * (1.0 - 1e-3) <= h.dist) {
                 DIAG(14);  // (diagnostic build) lanes whose cluster is not pruned
-                const CluSph* cs = p.csph + c * CLU_SIZE;
+                // leaves of CLU_SIZE_D, or CLU_SIZE for the scenes that need more than
+                // CLU_MAX of those (unrolled as one CLU_SIZE loop: a runtime trip count made
+                // the PATH64 cull kernel spill, A/B +10..17%)
+                const CluSph* cs = p.csph + c * p.clu_ls;
 #pragma unroll
                 for (int k = 0; k < CLU_SIZE; ++k) {
+                    if (k == CLU_SIZE_D && p.clu_ls == CLU_SIZE_D) break;
                     const int s = cs[k].slot;
                     if (s >= 0) sphere_exact<false>(cs[k].c, s, r, h, &p);
                 }

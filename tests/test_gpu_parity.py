@@ -505,12 +505,14 @@ def test_sphere_clusters_are_output_invariant(rend, prec):
     (-2000) and at the default, frames are bitwise those of the linear scan — with
     duplicated spheres (exact ties across clusters: the lower scene index must win), cameras
     inside the sphere cloud and far outside it (origins past the box margin's range test
-    every cluster unpruned), deep bounces."""
+    every cluster unpruned), deep bounces.  The fp64 kernels' leaves hold CLU_SIZE_D = 4
+    spheres up to 256 spheres (trial 5: 256, 64 full leaves) and fall back to the F32
+    kernels' 8 beyond (trial 3: 259)."""
     rng = np.random.default_rng(23)
     try:
         # trial 3: camera far outside the cloud but within the box margin's range (pruned
         # walk); trial 4: beyond 100x the scene extent (clu_oinf), every cluster unpruned
-        for trial, ns in enumerate((24, 70, 129, 256, 200)):
+        for trial, ns in enumerate((24, 70, 129, 256, 200, 253)):
             sc = scenes.synthetic_scene(ns, int(rng.integers(0, 7)),
                                         seed=int(rng.integers(1 << 30)))
             sph = [o for o in sc if o.kind == capi.RT_PRIM_SPHERE]
@@ -519,7 +521,7 @@ def test_sphere_clusters_are_output_invariant(rend, prec):
                 sc.append(scenes.Sphere(scenes.Material(tuple(rng.uniform(0, 1, 3)), .6),
                                         o.position, o.radius))
             rend.set_scene(scenes.to_prims(sc))
-            far = trial >= 3
+            far = trial in (3, 4)
             pos = (np.array([-400.0, 30.0, 10.0]) if trial == 3 else
                    np.array([-5000.0, 40.0, 12.0]) if trial == 4 else
                    rng.uniform([2, -3, -1], [8, 3, 2]))
