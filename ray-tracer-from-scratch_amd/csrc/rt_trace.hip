@@ -795,16 +795,36 @@ __device__ __forceinline__ void sphere_by_index(const KParams& p, int s, const R
     if (MIXED && sphere_cull(Sf, rf)) return;
     sphere_exact(p.s64[s >> 2].v[s & 3], s, r, h);
 }
-template <bool MIXED, bool EYE = false>
+#ifndef RT_WALL_SLOAD  // 1: the cull kernels' wall records through scalar loads (asm)
+#define RT_WALL_SLOAD 1
+#endif
+/* Wall w's fp64 record as two s_load_dwordx16 (the cull kernels: see clusters_mask's box
+ * loads for why the compiler's own loads there go through the vector memory path). */
+__device__ __forceinline__ Wall64 wall64_sload(const Wall64* q) {
+    typedef int v16i __attribute__((ext_vector_type(16)));
+    struct Two {
+        v16i a, b;
+    } t;
+    asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx16 %1, %2, 0x40\n\t"
+                 "s_waitcnt lgkmcnt(0)"
+                 : "=s"(t.a), "=s"(t.b)
+                 : "s"(q)
+                 : "memory");
+    return __builtin_bit_cast(Wall64, t);
+}
+template <bool MIXED, bool EYE = false, bool SL = false>
 __device__ __forceinline__ void walls_d(const KParams& p, const RayD& r, const RayF& rf, HitD& h) {
     for (int w = 0; w < p.nW; ++w) {
-        if (!MIXED && RT_WALL_PAIRS && w + 1 < p.nW) {
+        if (!MIXED && !SL && RT_WALL_PAIRS && w + 1 < p.nW) {
             wall_pair<EYE>(p, w, w + 1, r, h);
             ++w;
             continue;
         }
         if (MIXED && wall_cull(p.w32[w], rf)) continue;
-        wall_exact<EYE>(p.w64[w], w, p, r, h);
+        if (SL)
+            wall_exact<EYE>(wall64_sload(p.w64 + w), w, p, r, h);
+        else
+            wall_exact<EYE>(p.w64[w], w, p, r, h);
     }
 }
 
@@ -853,7 +873,10 @@ __device__ __forceinline__ void walls_d_kept(const KParams& p, const RayD& r, co
         const int w = __builtin_ctzll(wm);
         wm &= wm - 1;
         if (MIXED && wall_cull(p.w32[w], rf)) continue;
-        wall_exact<false>(p.w64[w], w, p, r, h);
+        if (RT_WALL_SLOAD)
+            wall_exact<false>(wall64_sload(p.w64 + w), w, p, r, h);
+        else
+            wall_exact<false>(p.w64[w], w, p, r, h);
     }
 }
 
@@ -1226,6 +1249,9 @@ __device__ __forceinline__ int clu_bit(const Clu32& B, int oct, int c) {
 #ifndef RT_CLU_SCHED
 #define RT_CLU_SCHED 1
 #endif
+#ifndef RT_CLU_SLOAD  // 1: the box pass's boxes through scalar loads (asm), see clusters_mask
+#define RT_CLU_SLOAD 1
+#endif
 #ifndef RT_CULL_WALL_CONE  // 1: the cull kernels' bounce segments test only the walls whose
 #define RT_CULL_WALL_CONE 1 // circumscribed ball meets the wave's cone (wall_cone_mask)
 #endif
@@ -1281,8 +1307,28 @@ __device__ __forceinline__ uint64_t clusters_mask(const KParams& p, const SlabRa
     const int n4 = (p.nclu + 3) & ~3;
     for (int c0 = 0; c0 < n4; c0 += RT_CLU_UNROLL) {
         Clu32 Bs[RT_CLU_UNROLL];  // wave-uniform: one batch of scalar loads
+#if RT_CLU_SLOAD
+        // the compiler cannot prove that nothing in the cull kernels writes the boxes (the
+        // DPP asm, the LDS stack), so it loads them through the vector memory path, one VMEM
+        // round trip per iteration; read here as two s_load_dwordx8 instead (reads through
+        // the scalar cache; the scene is constant while a kernel runs)
+        static_assert(RT_CLU_UNROLL == 2 && sizeof(Clu32) == 32, "two 32-byte boxes per batch");
+        {
+            typedef int v8i __attribute__((ext_vector_type(8)));
+            v8i r0, r1;
+            const Clu32* q = p.clu + c0;
+            asm volatile("s_load_dwordx8 %0, %2, 0x0\n\ts_load_dwordx8 %1, %2, 0x20\n\t"
+                         "s_waitcnt lgkmcnt(0)"
+                         : "=s"(r0), "=s"(r1)
+                         : "s"(q)
+                         : "memory");
+            Bs[0] = __builtin_bit_cast(Clu32, r0);
+            Bs[1] = __builtin_bit_cast(Clu32, r1);
+        }
+#else
 #pragma unroll
         for (int u = 0; u < RT_CLU_UNROLL; ++u) Bs[u] = p.clu[c0 + u];
+#endif
 #pragma unroll
         for (int u = 0; u < RT_CLU_UNROLL; ++u) {
             // one box at a time (a handful of VGPRs), not four interleaved
@@ -1368,7 +1414,7 @@ __device__ __forceinline__ HitD scan_d(const KParams& p, const RayD& r, bool ali
                 if (wm != ~0ull)
                     walls_d_kept<MIXED>(p, r, rf, h, wm);
                 else
-                    walls_d<MIXED>(p, r, rf, h);
+                    walls_d<MIXED, false, RT_WALL_SLOAD>(p, r, rf, h);
             }
         }
         // a wide cone (live rays pointing everywhere) culls little: each lane its own clusters
