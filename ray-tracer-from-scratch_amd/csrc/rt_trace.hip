@@ -2134,11 +2134,25 @@ __device__ __forceinline__ void sphere_pair_f(const SphG32& G, int k0, int s0, i
     }
 }
 
+/* A 64-byte record (Wall32, SphG32) as one s_load_dwordx16: the F32 cull kernels' walls and
+ * cone survivors (see clusters_mask's box loads). */
+template <class T>
+__device__ __forceinline__ T rec64_sload(const T* q) {
+    static_assert(sizeof(T) == 64, "one s_load_dwordx16");
+    typedef int v16i __attribute__((ext_vector_type(16)));
+    v16i a;
+    asm volatile("s_load_dwordx16 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)"
+                 : "=s"(a)
+                 : "s"(q)
+                 : "memory");
+    return __builtin_bit_cast(T, a);
+}
+template <bool SL = false>
 __device__ __forceinline__ void walls_f(const KParams& p, f3 o, f3 d, float& best, int& slot,
                                         uint64_t wmask = ~0ull) {
     for (int w = 0; w < p.nW; ++w) {
         if (w < 64 && !((wmask >> w) & 1)) continue;  // wave-uniform (tile bins)
-        const Wall32& Wl = p.w32[w];
+        const Wall32 Wl = SL ? rec64_sload(p.w32 + w) : p.w32[w];
         const f3 nw = F3(Wl.n[0], Wl.n[1], Wl.n[2]), P = F3(Wl.P[0], Wl.P[1], Wl.P[2]);
         const float den = fdot(nw, d);
         const float num = fdot(P - o, nw);
@@ -2235,7 +2249,7 @@ __device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, bool
                 uint64_t wm = k == 0 ? wkeep : ~0ull;
                 if (RT_CULL_WALL_CONE && k > 0 && cn.on && p.nW > 0 && p.nW <= 64)
                     wm = wall_cone_mask(p, cn);
-                if (alive) walls_f(p, o, d, best, slot, wm);
+                if (alive) walls_f<RT_WALL_SLOAD>(p, o, d, best, slot, wm);
             }
             // wide cone: each lane its own sphere clusters (clusters_scan)
             const bool clusters = RT_CLUSTERS_F32 && p.nclu > 0 && cn.cos_t < p.clu_cos;
@@ -2257,6 +2271,7 @@ __device__ __forceinline__ f3 trace_pixel_f(const KParams& p, int x, int i, bool
                             Sf[2] = lane_f(rec.f[2], l);
                             Sf[3] = lane_f(rec.f[3], l);
                         } else {
+                            // (not through rec64_sload: a wait per survivor, c5 +31%)
                             const SphG32& G = p.s32[sidx >> 2];
                             Sf[0] = G.c[0][sidx & 3];
                             Sf[1] = G.c[1][sidx & 3];
