@@ -128,6 +128,11 @@ def load_profile(path: str, workload: str, precision: str):
 
 
 def main() -> int:
+    # stdout carries the ONE JSON line: anything the libraries print there (RCCL's version
+    # banner when a communicator is made) goes to stderr, the JSON to a private copy of fd 1
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawTextHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -149,6 +154,11 @@ def main() -> int:
                          "rtamd.tiling over torch.distributed")
     ap.add_argument("--transport", default="rccl", choices=["rccl", "copy"],
                     help="rt_multi transport (copy: one process only, --local-ranks)")
+    ap.add_argument("--band-layout", default="weighted", choices=["equal", "weighted"],
+                    help="tiled mode, N > 1: rank r's rows of the frame — equal contiguous bands "
+                         "(rt_band_rows), or contiguous bands cut so each carries 1/N of the "
+                         "tile-row costs rank 0 measures once on its GPU and broadcasts "
+                         "(rt_weighted_band_rows, RT_OPT_MULTI_LAYOUT 2)")
     ap.add_argument("--local-ranks", type=int, default=1,
                     help="rehearsal only (one process): split the frame over this many ranks "
                          "on this one GPU with the peer-copy transport; not a measurement")
@@ -222,8 +232,20 @@ def main() -> int:
     cam_fly = capi.camera_init(**scenes.camera_args(cfg.width, cfg.height))
     cam_fly.position[0] += 0.1 * rank
     cam = cam0 if tiled_mode else cam_fly
-    # this rank's rows: its band of the one frame (tiled), or the whole frame (frames)
-    if tiled_mode:
+    # this rank's rows: its band of the one frame (tiled), or the whole frame (frames).
+    # Weighted bands: rank 0 measures every tile row's cost on one full render of the frame
+    # (untimed, rt_tile_row_costs) and broadcasts it, so every rank cuts the same bands.
+    layout = {"equal": 0, "weighted": 2}[args.band_layout] \
+        if (world > 1 or args.local_ranks > 1) else 0
+    weights = None
+    if tiled_mode and layout == 2:
+        w_ = [rend.tile_row_costs(cam0, depth, prec, flags).tolist() if rank == 0 else None]
+        if world > 1:
+            dist.broadcast_object_list(w_, src=0)
+        weights = w_[0]
+    if tiled_mode and layout == 2:
+        row0, nrows = capi.weighted_band_rows(H, world, rank, weights)
+    elif tiled_mode:
         row0, nrows = capi.band_rows(H, world, rank)
     else:
         row0, nrows = 0, H
@@ -269,6 +291,9 @@ def main() -> int:
         multi.set_option(capi.RT_OPT_BOX_CACHE, args.box_cache)
         multi.set_option(capi.RT_OPT_ROW_FEEDBACK, args.row_feedback)
         multi.set_scene(prims)
+        if layout == 2:
+            multi.set_row_weights(weights)
+        multi.set_option(capi.RT_OPT_MULTI_LAYOUT, layout)
     elif tiled_mode:
         from rtamd import tiling
         # double-buffered: the gather of frame k (collective stream) overlaps the render of k+1
@@ -291,15 +316,36 @@ def main() -> int:
             rend.render_device(cam, depth, ref.data_ptr(), prec, flags, out_fmt,
                                stream=stream.cuda_stream)
         got = None
-        if multi is not None:
+        chk = multi
+        op_name = None
+        if multi is not None and world == 1 and multi.nranks == 1:
+            # one GPU: the timed operator renders the frame in place (no communicator); check
+            # the gather's RCCL calls here instead, untimed, through a one-rank loopback
+            # communicator (the root's band sent to itself: ncclCommInitRank, the group,
+            # ncclSend/ncclRecv, ncclCommGetAsyncError all run)
+            chk = capi.MultiRenderer([local], transport=capi.RT_TRANSPORT_RCCL_LOOPBACK)
+            chk.set_option(capi.RT_OPT_ROW_FEEDBACK, args.row_feedback)
+            chk.set_scene(prims)
+            op_name = ("rt_multi, RT_TRANSPORT_RCCL_LOOPBACK: RCCL send/recv of the one band "
+                       "through a one-rank communicator (the timed N = 1 loop renders in place)")
+        elif multi is not None:
+            op_name = (f"rt_multi, {multi.nranks} ranks, "
+                       + ("RCCL send/recv" if args.transport == "rccl" and world > 1
+                          else "peer copies (rehearsal)")
+                       + f", {args.band_layout} bands")
+        if chk is not None:
             outs[0].fill_(-1.0)
             torch.cuda.synchronize(dev)
-            multi.render_device_frames([cam], depth, out_ptrs[:1] if multi.has_root else [], prec,
-                                       flags, out_fmt, streams=st_ptrs[:1], nframes=1)
+            # three frames in flight over two buffers: buffer 0 ends with the third
+            chk.render_device_frames([cam], depth, out_ptrs[:2] if chk.has_root else [], prec,
+                                     flags, out_fmt, streams=st_ptrs[:2] if chk.has_root else st_ptrs[:1],
+                                     nframes=3 if len(out_ptrs) > 1 else 1)
             torch.cuda.synchronize(dev)
-            multi.sync()
+            chk.sync()
             if rank == 0:
                 got = outs[0].view(torch.uint8).flatten()[:nbytes]
+            if chk is not multi:
+                chk.close()
         elif torch_tiled is not None:
             h_ = torch_tiled.submit()
             torch_tiled.wait(h_)
@@ -312,7 +358,7 @@ def main() -> int:
             eq = bool(torch.equal(got, ref.view(torch.uint8).flatten()[:nbytes]))
             gather_check = {"bitwise_equal_to_one_gpu_frame": eq, "ranks": world,
                             "output": args.out,
-                            "operator": "rt_multi (RCCL send/recv)" if multi is not None
+                            "operator": op_name if multi is not None
                             else "rtamd.tiling (torch.distributed gather)"}
             if not eq:
                 print(f"bench: the gathered {world}-rank frame differs from the one-GPU frame",
@@ -661,6 +707,7 @@ def main() -> int:
                 "segments_per_pixel": round(total_segs / px_step, 4),
                 "parallelism": par,
                 "band_rows_rank0": nrows,
+                "band_layout": args.band_layout if (tiled_mode and (world > 1 or args.local_ranks > 1)) else None,
                 "host_box_cache": bool(args.box_cache),
                 "row_feedback": args.row_feedback,
                 "frames_in_flight": fif,
@@ -707,7 +754,7 @@ def main() -> int:
         }
         if world == 1 and not args.no_cpu_baseline and args.cpu_seconds > 0:
             result["cpu_baseline"] = cpu_baseline(cfg, prims, cam0, depth, flags, args.cpu_seconds)
-        print(json.dumps(result), flush=True)
+        print(json.dumps(result), file=json_out, flush=True)
     if multi is not None:
         multi.close()
     rend.close()

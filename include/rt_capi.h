@@ -201,17 +201,23 @@ enum rt_option {
                                          band's snapshots, acc = W% acc + (100-W)% new;
                                          0 = the latest snapshot alone.  Output is
                                          identical. */
-    RT_OPT_ROW_FEEDBACK_ISOLATE = 15, /* 1 (default): a frame whose tile costs
-                                         RT_OPT_ROW_FEEDBACK samples runs alone on the GPU
-                                         (its stream waits for this ctx's frames on other
-                                         streams, and their next frames wait for it), so the
-                                         costs are not those of overlapping frames; 0 = it
-                                         overlaps like any frame.  Output is identical. */
+    RT_OPT_ROW_FEEDBACK_ISOLATE = 15, /* 1: a frame whose tile costs RT_OPT_ROW_FEEDBACK
+                                         samples runs alone on the GPU (its stream waits for
+                                         this ctx's frames on other streams, and their next
+                                         frames wait for it), so the costs are not those of
+                                         overlapping frames; 0 (default) = it overlaps like
+                                         any frame (measured: the lost overlap costs more
+                                         than cleaner costs gain).  Output is identical. */
     RT_OPT_MULTI_LAYOUT = 13,        /* rt_multi_set_option only: 0 (default) = contiguous
                                          row bands (rt_band_rows); 1 = interleaved tile rows
                                          (rt_interleaved_rows): balanced when the frame's cost
-                                         is concentrated in some rows (config 5).  The
-                                         gathered frame is identical. */
+                                         is concentrated in some rows (config 5); 2 =
+                                         contiguous bands cut at tile rows so that each
+                                         carries an equal share of the per-tile-row weights
+                                         given to rt_multi_set_row_weights
+                                         (rt_weighted_band_rows; equal bands while no weights
+                                         cover the frame's tile rows).  The gathered frame is
+                                         identical. */
     RT_OPT_CLUSTER_COS = 12           /* C in [-2000, 2000] (default 400): in scenes that use
                                          the wave cull, a wave (any precision) whose live
                                          rays' cone has cos(half-angle) < C/1000 tests each
@@ -285,17 +291,31 @@ int rt_render_device_frames(rt_ctx* ctx, const rt_camera* cams, int32_t ncams, i
  * its render stream while the previous frame's band is still being sent on its comm stream;
  * a band buffer is reused only after its send has completed (device-side event waits; the
  * host never blocks in rt_multi_render_device*).
- * Failures: a frame that fails on one rank after another rank may already have queued its
- * part of the gather leaves the communicator out of step; the rt_multi is then broken —
- * every later frame returns RT_ERR_COMM, rt_multi_sync aborts the communicator
+ * Failures: a frame that fails on one rank after a local rank has queued its part of the
+ * gather (a receive or a send) leaves the communicator out of step; the rt_multi is then
+ * broken — every later frame returns RT_ERR_COMM, rt_multi_sync aborts the communicator
  * (ncclCommAbort) instead of waiting on receives that cannot complete, and
- * rt_multi_destroy aborts instead of destroying. */
+ * rt_multi_destroy aborts instead of destroying.  A frame that fails before any local
+ * rank queued anything (no scene, an unsupported combination) returns its status and leaves
+ * the rt_multi usable.  With one process per GPU this is local to the process that saw the
+ * failure: the other processes are not told, and their sends, receives or rt_multi_sync can
+ * block until their own communicator is aborted (RT_TRANSPORT_THREADS does tell its peers). */
 #define RT_MULTI_ID_BYTES 128
 #define RT_MULTI_SLOTS 2
 enum rt_transport {
     RT_TRANSPORT_RCCL = 0,
     RT_TRANSPORT_COPY = 1,
-    RT_TRANSPORT_RCCL_LOOPBACK = 2
+    RT_TRANSPORT_RCCL_LOOPBACK = 2,
+    /* Rehearsal of the one-process-per-GPU model inside ONE process: every rank is its own
+     * rt_multi handle (nlocal = 1, first_rank = its rank, the same unique_id, which keys an
+     * in-process mailbox), each driven from its own thread as a separate process would drive
+     * it, and each ncclSend/ncclRecv pair is a peer copy matched through the mailbox (the
+     * root posts where the part lands and after which event; the sender's comm stream waits
+     * for it, copies, and posts its completion event, which the root's comm stream waits
+     * on).  Handles may share a device.  The host calls of a frame block until the peer's
+     * matching post (RCCL's never block); a handle's failure or destroy ends the exchange
+     * for all of them (RT_ERR_COMM, no hang). */
+    RT_TRANSPORT_THREADS = 3
 };
 typedef struct rt_multi rt_multi;
 
@@ -344,7 +364,26 @@ int rt_multi_render(rt_multi* m, const rt_camera* cam, int32_t depth, int32_t pr
  * asynchronous error. */
 int rt_multi_sync(rt_multi* m);
 
-/* Interleaved parts: the frame's tile rows (8 pixel rows each; the last may be shorter)
+/* Per-tile-row weights (n = tile rows of the frames to come, rt_tile_rows() pixel rows each)
+ * for RT_OPT_MULTI_LAYOUT = 2, e.g. rt_tile_row_costs of one GPU's render of the frame.
+ * Every rank must be given the same weights (one process per GPU: broadcast them).  n = 0
+ * clears them.  Frames in flight keep the bands they started with. */
+int rt_multi_set_row_weights(rt_multi* m, const float* weights, int32_t n);
+
+/* Contiguous band of `rank` whose boundaries fall on tile rows: boundary r (0 < r < nranks)
+ * is the tile row t whose prefix sum of weights[0..t) is nearest r/nranks of the total (ties
+ * to the lower t; boundaries never decrease).  weights must hold one entry >= 0 per tile row
+ * of `height` (n == ceil(height / rt_tile_rows())); otherwise RT_ERR_INVALID_ARG. */
+int rt_weighted_band_rows(int32_t height, int32_t nranks, int32_t rank, const float* weights,
+                          int32_t n, int32_t* row0, int32_t* nrows);
+
+/* Measured cost of every tile row of the frame (synchronous): one render of the whole frame
+ * by the stamped kernels, in which every wave records its shader cycles; costs[t] = the sum
+ * over tile row t's waves in units of 32 cycles.  n must be ceil(height / rt_tile_rows()). */
+int rt_tile_row_costs(rt_ctx* ctx, const rt_camera* cam, int32_t depth, int32_t precision,
+                      uint32_t flags, float* costs, int32_t n);
+
+/* Interleaved parts: the frame's tile rows (rt_tile_rows() = 8 pixel rows each; the last may be shorter)
  * dealt round-robin to nparts parts — part p owns tile rows p, p + nparts, p + 2 nparts, ...
  * — so every part gets a share of the frame's heavy and light rows (rt_multi's balanced
  * layout, RT_OPT_MULTI_LAYOUT).  *nrows = the part's pixel rows. */

@@ -97,7 +97,7 @@ struct rt_ctx {
     int cost_ul = 0;               // units per tile row (log2) of the pending snapshot
     hipEvent_t ev_cost = nullptr;  // snapshot landed
     bool cost_pending = false;
-    // RT_OPT_ROW_FEEDBACK_ISOLATE (default 1): a sampled frame runs alone on the GPU — its
+    // RT_OPT_ROW_FEEDBACK_ISOLATE (default 0): a sampled frame runs alone on the GPU — its
     // stream waits for the other streams' latest frames, and each other stream's next frame
     // waits for it — so its wave costs are not those of two frames sharing the CUs (frames
     // in flight overlap a frame's tail with the next one's start, which inflated or hid the
@@ -1619,3 +1619,51 @@ int rt_render(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nrows, in
 }
 
 }  // extern "C"
+
+int rt_tile_row_costs(rt_ctx* ctx, const rt_camera* cam, int32_t depth, int32_t precision,
+                      uint32_t flags, float* costs, int32_t n) {
+    const int32_t H = cam ? cam->height : 0;
+    int st = check_render_args(ctx, cam, 0, H, depth, precision, RT_OUT_RGB_F32);
+    if (st != RT_OK) return st;
+    const int gy = (H + rt::TILE_H - 1) / rt::TILE_H;
+    if (!costs || n != gy) return RT_ERR_INVALID_ARG;
+    if (gy == 0 || cam->width == 0) {
+        for (int t = 0; t < n; t++) costs[t] = 0.0f;
+        return RT_OK;
+    }
+    DeviceGuard dg(ctx->device);
+    RT_HIP(ctx, dg.err);
+    const int per_row = ((cam->width + rt::TILE_W - 1) / rt::TILE_W) * (rt::BLOCK / 64);
+    const size_t nw = (size_t)gy * per_row;
+    const size_t out_bytes = (size_t)H * cam->width * 12;
+    // scratch for this call only (the frame's pixels and every wave's cost)
+    void* d_img = nullptr;
+    uint16_t* d_c = nullptr;
+    std::vector<uint16_t> h_c(nw);
+    auto release = [&] {
+        if (d_img) (void)hipFree(d_img);
+        if (d_c) (void)hipFree(d_c);
+    };
+    hipError_t e = hipMalloc(&d_img, out_bytes);
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d_c), nw * sizeof(uint16_t));
+    if (e == hipSuccess) e = hipMemsetAsync(d_c, 0, nw * sizeof(uint16_t), ctx->stream);
+    if (e != hipSuccess) {
+        release();
+        return hip_fail(ctx, e, "rt_tile_row_costs buffers");
+    }
+    rt::KParams p = make_params(ctx, cam, 0, H, depth, flags, RT_OUT_RGB_F32, d_img, nullptr, precision);
+    p.pairs = 0;        // one tile per wave: costs[t] sums tile row t's waves
+    p.tile_cost = d_c;  // the stamped kernels
+    const int le = rt::launch_trace(p, precision, ctx->stream);
+    if (le == (int)hipSuccess) e = hipMemcpyAsync(h_c.data(), d_c, nw * sizeof(uint16_t), hipMemcpyDeviceToHost, ctx->stream);
+    if (le == (int)hipSuccess && e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    release();
+    if (le != (int)hipSuccess) return hip_fail(ctx, (hipError_t)le, "launch k_trace (stamped)");
+    if (e != hipSuccess) return hip_fail(ctx, e, "rt_tile_row_costs copy");
+    for (int t = 0; t < gy; t++) {
+        double s = 0.0;
+        for (int k = 0; k < per_row; k++) s += h_c[(size_t)t * per_row + k];
+        costs[t] = (float)s;
+    }
+    return RT_OK;
+}

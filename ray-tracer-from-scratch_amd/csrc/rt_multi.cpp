@@ -23,6 +23,16 @@
  * One process driving several GPUs runs the extra ranks' host work (pixel boxes, row order,
  * launch: rt_render_device) on one worker thread per rank, in parallel with the caller's
  * thread, which does the root's.
+ *
+ * RT_TRANSPORT_THREADS (rehearsal): the process-per-GPU structure — one rt_multi handle per
+ * rank, nlocal = 1, non-root handles without a frame buffer — with the handles living in ONE
+ * process, each driven from its own thread, and every ncclSend/ncclRecv pair replaced by a
+ * peer copy matched through an in-process mailbox (Hub, keyed by the unique id): the root
+ * posts where frame k's part of rank g lands and the event after which it may be written;
+ * the sender's comm stream waits for that event, copies, and posts its completion event, on
+ * which the root's comm stream waits.  So a one-GPU box runs every branch a process-per-GPU
+ * RCCL run takes (the non-root enqueue, the caller-stream wait on the send, the root's
+ * interleaved staging and scatter) except the RCCL calls themselves.
  */
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -34,7 +44,10 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <map>
+#include <memory>
 #include <mutex>
+#include <string>
 #include <new>
 #include <thread>
 #include <vector>
@@ -69,7 +82,8 @@ struct Rank {
     size_t band_cap = 0;
     hipEvent_t ev_rendered[RT_MULTI_SLOTS] = {nullptr, nullptr};
     hipEvent_t ev_sent[RT_MULTI_SLOTS] = {nullptr, nullptr};
-    hipEvent_t ev_done = nullptr;   // root, RCCL: every band received
+    hipEvent_t ev_done = nullptr;   // root, RCCL / THREADS: every band received
+    hipEvent_t ev_ready[RT_MULTI_SLOTS] = {nullptr, nullptr};  // root, THREADS: parts may land
     // root, RCCL, interleaved layout: every rank's part received here, then scattered into
     // its frame rows (one strided copy per part)
     void* staging[RT_MULTI_SLOTS] = {nullptr, nullptr};
@@ -84,11 +98,33 @@ struct Rank {
     int status = RT_OK;
 };
 
+/* RT_TRANSPORT_THREADS mailbox shared by the handles of one unique id (see the file
+ * comment).  Keys are (frame number of the handles, sending rank): every handle counts the
+ * frames it renders, and the handles of one exchange render the same sequence. */
+struct Post {
+    void* dst = nullptr;      // root: where the part lands
+    int device = 0;           // root's device
+    size_t bytes = 0;
+    hipEvent_t ev = nullptr;  // root -> sender: the destination may be written after it;
+                              // sender -> root: the copy is complete after it
+};
+struct Hub {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::map<std::pair<uint64_t, int>, Post> recv, sent;
+    int refs = 0;
+    bool failed = false;      // a handle failed mid-exchange or was destroyed: waits give up
+};
+std::mutex g_hubs_mu;
+std::map<std::string, std::shared_ptr<Hub>> g_hubs;
+
 }  // namespace
 
 struct rt_multi {
     int nranks = 1, nlocal = 1, first_rank = 0, transport = RT_TRANSPORT_RCCL;
-    int layout = 0;                 // RT_OPT_MULTI_LAYOUT: 0 contiguous bands, 1 interleaved
+    int layout = 0;                 // RT_OPT_MULTI_LAYOUT: 0 contiguous bands, 1 interleaved,
+                                    // 2 contiguous bands weighted by `weights`
+    std::vector<float> weights;     // rt_multi_set_row_weights: per tile row
     std::vector<Rank*> r;           // local ranks, r[0] = first_rank
     uint64_t frame = 0;
     hipEvent_t ev_in[RT_MULTI_SLOTS] = {nullptr, nullptr};  // root's device (process with root)
@@ -100,11 +136,18 @@ struct rt_multi {
     // a frame failed after some rank may have queued its part of the gather: the
     // communicator is out of step (see rt_capi.h); `aborted` once ncclCommAbort has run
     bool broken = false, aborted = false;
+    // set once any local rank has queued its part of this frame's exchange (a receive, a send
+    // or a mailbox post): only a failure after that leaves the peers out of step
+    std::atomic<bool> queued{false};
+    std::shared_ptr<Hub> hub;       // RT_TRANSPORT_THREADS
+    std::string hub_key;
     bool has_root() const { return first_rank == 0; }
-    bool rccl() const { return transport != RT_TRANSPORT_COPY; }
+    bool rccl() const { return transport == RT_TRANSPORT_RCCL || transport == RT_TRANSPORT_RCCL_LOOPBACK; }
     bool loopback() const { return transport == RT_TRANSPORT_RCCL_LOOPBACK; }
-    // the frame goes through a communicator (several ranks, or the root's band to itself)
-    bool gathers() const { return rccl() && (nranks > 1 || loopback()); }
+    bool threads() const { return transport == RT_TRANSPORT_THREADS; }
+    // the frame goes through an exchange between ranks (a communicator with several ranks or
+    // the root's band to itself, or the THREADS mailbox); COPY writes the root's frame directly
+    bool gathers() const { return (rccl() && (nranks > 1 || loopback())) || threads(); }
 };
 
 namespace {
@@ -181,7 +224,57 @@ struct SlowCall {
 
 int bpp(int32_t f) { return rt_out_bytes_per_pixel(f); }
 
-/* Band buffers of a non-root rank, grown (rarely) to `bytes` each. */
+/* ---- RT_TRANSPORT_THREADS mailbox ---- */
+int hub_timeout_ms() {
+    static const int ms = [] {
+        const char* e = std::getenv("RT_MULTI_THREADS_TIMEOUT_MS");
+        const int v = e ? std::atoi(e) : 0;
+        return v > 0 ? v : 30000;
+    }();
+    return ms;
+}
+void hub_fail(rt_multi* m) {
+    if (!m->hub) return;
+    {
+        std::lock_guard<std::mutex> lk(m->hub->mu);
+        m->hub->failed = true;
+    }
+    m->hub->cv.notify_all();
+}
+void hub_put(rt_multi* m, std::map<std::pair<uint64_t, int>, Post> Hub::*box, uint64_t frame, int rank,
+             const Post& p) {
+    {
+        std::lock_guard<std::mutex> lk(m->hub->mu);
+        (m->hub.get()->*box)[{frame, rank}] = p;
+    }
+    m->hub->cv.notify_all();
+}
+/* Blocks until the peer has posted (frame, rank) into `box`, then takes the post. */
+int hub_take(rt_multi* m, std::map<std::pair<uint64_t, int>, Post> Hub::*box, uint64_t frame, int rank,
+             Post* out, const char* what) {
+    Hub& h = *m->hub;
+    std::unique_lock<std::mutex> lk(h.mu);
+    auto& mp = h.*box;
+    const bool ok = h.cv.wait_for(lk, std::chrono::milliseconds(hub_timeout_ms()), [&] {
+        return h.failed || mp.count({frame, rank}) != 0;
+    });
+    auto it = mp.find({frame, rank});
+    if (it == mp.end()) {
+        std::snprintf(m->last_err, sizeof m->last_err, "%s (frame %llu, rank %d): %s", what,
+                      (unsigned long long)frame, rank,
+                      ok ? "a peer handle failed or was destroyed" : "timed out");
+        return RT_ERR_COMM;
+    }
+    *out = it->second;
+    mp.erase(it);
+    return RT_OK;
+}
+
+/* Band buffers of a rank, grown (rarely) to `bytes` each: a non-root rank renders into them
+ * on its render streams; the root does too under RT_TRANSPORT_RCCL_LOOPBACK, on the CALLER's
+ * stream.  Draining the render and comm streams also covers those caller-stream renders:
+ * every one is followed by a comm-stream wait on ev_rendered[s] before its self-send, so the
+ * comm stream completes only after them. */
 int ensure_bands(rt_multi* m, Rank* k, size_t bytes) {
     if (bytes <= k->band_cap) return RT_OK;
     // nothing in flight may still read or write the old buffers
@@ -205,6 +298,10 @@ Part part_of(const rt_multi* m, int32_t height, int rank) {
     Part pt;
     if (m->layout == 1 && m->nranks > 1)
         (void)rt_interleaved_rows(height, m->nranks, rank, &pt.nrows);
+    else if (m->layout == 2 && m->nranks > 1 &&
+             rt_weighted_band_rows(height, m->nranks, rank, m->weights.data(), (int32_t)m->weights.size(),
+                                   &pt.row0, &pt.nrows) == RT_OK)
+        ;  // weighted bands (equal bands below while the weights do not cover this frame)
     else
         (void)rt_band_rows(height, m->nranks, rank, &pt.row0, &pt.nrows);
     return pt;
@@ -283,6 +380,7 @@ int enqueue_rank(rt_multi* m, Rank* k, const Job& j) {
             if (st != RT_OK) return st;
         }
         if (m->gathers()) {
+            m->queued.store(true, std::memory_order_relaxed);
             const size_t part_bytes = (size_t)max_part_rows(m, cam.height) * row_bytes;
             if (inter && part_bytes * m->nranks > k->staging_cap) {
                 // grow (rare): the comm stream may still scatter from the old buffers
@@ -296,6 +394,38 @@ int enqueue_rank(rt_multi* m, Rank* k, const Job& j) {
                 k->staging_cap = part_bytes * m->nranks;
             }
             MHIPF(m, hipStreamWaitEvent(k->comm_stream, j.ev_in, 0));
+            if (m->threads()) {
+                // the mailbox's receives: post where every part lands (after ev_ready: the
+                // caller's earlier work on the frame is done), then wait on each part's copy
+                MHIPF(m, hipEventRecord(k->ev_ready[s], k->comm_stream));
+                for (int g = 1; g < m->nranks; g++) {
+                    const Part pg = part_of(m, cam.height, g);
+                    if (pg.nrows <= 0 || row_bytes == 0) continue;
+                    Post p;
+                    p.dst = inter ? static_cast<char*>(k->staging[s]) + (size_t)g * part_bytes
+                                  : j.d_frame + (size_t)pg.row0 * row_bytes;
+                    p.device = k->device;
+                    p.bytes = (size_t)pg.nrows * row_bytes;
+                    p.ev = k->ev_ready[s];
+                    hub_put(m, &Hub::recv, m->frame, g, p);
+                }
+                for (int g = 1; g < m->nranks; g++) {
+                    const Part pg = part_of(m, cam.height, g);
+                    if (pg.nrows <= 0 || row_bytes == 0) continue;
+                    Post p;
+                    st = hub_take(m, &Hub::sent, m->frame, g, &p, "waiting for a part's copy");
+                    if (st != RT_OK) return st;
+                    MHIPF(m, hipStreamWaitEvent(k->comm_stream, p.ev, 0));
+                }
+                if (inter)
+                    for (int g = 1; g < m->nranks; g++) {
+                        st = scatter_part(m, j.d_frame, static_cast<char*>(k->staging[s]) + (size_t)g * part_bytes,
+                                          cam.height, g, row_bytes, k->comm_stream);
+                        if (st != RT_OK) return st;
+                    }
+                MHIPF(m, hipEventRecord(k->ev_done, k->comm_stream));
+                return RT_OK;
+            }
             if (lb) MHIPF(m, hipStreamWaitEvent(k->comm_stream, k->ev_rendered[s], 0));
             MNCCL(m, ncclGroupStart());
             if (lb) {
@@ -345,8 +475,25 @@ int enqueue_rank(rt_multi* m, Rank* k, const Job& j) {
     if (st != RT_OK) return st;
     MHIPF(m, hipEventRecord(k->ev_rendered[s], k->render_stream[s]));
     MHIPF(m, hipStreamWaitEvent(k->comm_stream, k->ev_rendered[s], 0));
+    m->queued.store(true, std::memory_order_relaxed);
     if (m->rccl()) {
         MNCCL(m, ncclSend(k->band[s], bytes, ncclUint8, 0, k->comm, k->comm_stream));
+    } else if (m->threads()) {
+        // the mailbox's send: where the root wants this part, once it may be written
+        Post p;
+        st = hub_take(m, &Hub::recv, m->frame, k->rank, &p, "waiting for the root's receive");
+        if (st != RT_OK) return st;
+        if (p.bytes != bytes) {
+            std::snprintf(m->last_err, sizeof m->last_err, "rank %d: the root expects %zu bytes, the part has %zu",
+                          k->rank, p.bytes, bytes);
+            return RT_ERR_COMM;
+        }
+        MHIPF(m, hipStreamWaitEvent(k->comm_stream, p.ev, 0));
+        MHIPF(m, hipMemcpyPeerAsync(p.dst, p.device, k->band[s], k->device, bytes, k->comm_stream));
+        MHIPF(m, hipEventRecord(k->ev_sent[s], k->comm_stream));
+        Post done;
+        done.ev = k->ev_sent[s];
+        hub_put(m, &Hub::sent, m->frame, k->rank, done);
     } else {
         // the root's rows may still be read by the caller's earlier work on the frame buffer
         MHIPF(m, hipStreamWaitEvent(k->comm_stream, j.ev_in, 0));
@@ -359,8 +506,10 @@ int enqueue_rank(rt_multi* m, Rank* k, const Job& j) {
                                        k->device, bytes, k->comm_stream));
         }
     }
-    MHIPF(m, hipEventRecord(k->ev_sent[s], k->comm_stream));
-    if (j.stream && m->rccl() && !m->has_root())
+    if (!m->threads()) MHIPF(m, hipEventRecord(k->ev_sent[s], k->comm_stream));  // THREADS: above
+    // a process without the root: work the caller enqueues later on its stream (on this
+    // rank's device) follows the band's send
+    if (j.stream && !m->has_root())
         MHIPF(m, hipStreamWaitEvent(j.stream, k->ev_sent[s], 0));
     return RT_OK;
 }
@@ -407,6 +556,8 @@ void destroy_rank(Rank* k, bool abort_comm) {
         if (k->ev_sent[s]) (void)hipEventDestroy(k->ev_sent[s]);
     }
     if (k->ev_done) (void)hipEventDestroy(k->ev_done);
+    for (auto& e : k->ev_ready)
+        if (e) (void)hipEventDestroy(e);
     for (auto& b : k->staging)
         if (b) (void)hipFree(b);
     for (auto rs : k->render_stream)
@@ -435,6 +586,7 @@ int render_frame(rt_multi* m, const rt_camera* cam, int32_t depth, int32_t preci
         return RT_ERR_COMM;
     }
     const int slot = (int)(m->frame % RT_MULTI_SLOTS);
+    m->queued.store(false, std::memory_order_relaxed);
     Job j;
     j.cam = cam;
     j.depth = depth;
@@ -478,14 +630,23 @@ int render_frame(rt_multi* m, const rt_camera* cam, int32_t depth, int32_t preci
     }
     m->frame++;
     if (st != RT_OK) {
-        if (m->gathers()) m->broken = true;  // another rank may have queued its send/recv
+        // out of step only if some rank already queued its part of the exchange (a failure
+        // before that — no scene, an unsupported combination — leaves the communicator
+        // usable); THREADS handles count frames in step, so any failure ends the exchange
+        // and wakes the peers' mailbox waits
+        if (m->threads()) {
+            m->broken = true;
+            hub_fail(m);
+        } else if (m->gathers() && m->queued.load(std::memory_order_relaxed)) {
+            m->broken = true;
+        }
         return st;
     }
     if (root && (m->nranks > 1 || m->gathers())) {
         // the caller's stream sees the complete frame
         DevGuard dg(root->device);
         MHIP(m, dg.err);
-        if (m->rccl()) {
+        if (m->rccl() || m->threads()) {
             MHIPF(m, hipStreamWaitEvent(j.stream, root->ev_done, 0));
         } else {
             for (int L = 1; L < m->nlocal; L++) MHIPF(m, hipStreamWaitEvent(j.stream, m->r[L]->ev_sent[slot], 0));
@@ -516,16 +677,18 @@ int rt_multi_create(const int32_t* devices, int32_t nlocal, int32_t nranks, int3
     if (!devices || nlocal <= 0 || nranks <= 0 || first_rank < 0 || first_rank + nlocal > nranks)
         return RT_ERR_INVALID_ARG;
     if (transport != RT_TRANSPORT_RCCL && transport != RT_TRANSPORT_COPY &&
-        transport != RT_TRANSPORT_RCCL_LOOPBACK)
+        transport != RT_TRANSPORT_RCCL_LOOPBACK && transport != RT_TRANSPORT_THREADS)
         return RT_ERR_INVALID_ARG;
     const bool one_process = nlocal == nranks;
     if (!one_process && (!unique_id || transport == RT_TRANSPORT_COPY))
         return transport == RT_TRANSPORT_COPY ? RT_ERR_UNSUPPORTED : RT_ERR_INVALID_ARG;
+    // THREADS: one handle per rank (the process-per-GPU shape), two ranks at least
+    if (transport == RT_TRANSPORT_THREADS && (nlocal != 1 || nranks < 2)) return RT_ERR_INVALID_ARG;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return RT_ERR_NO_DEVICE;
     for (int L = 0; L < nlocal; L++)
         if (devices[L] < 0 || devices[L] >= ndev) return RT_ERR_NO_DEVICE;
-    if (transport != RT_TRANSPORT_COPY)
+    if (transport != RT_TRANSPORT_COPY && transport != RT_TRANSPORT_THREADS)
         for (int a = 0; a < nlocal; a++)
             for (int b = a + 1; b < nlocal; b++)
                 if (devices[a] == devices[b]) return RT_ERR_UNSUPPORTED;  // RCCL: one rank per GPU
@@ -565,6 +728,7 @@ int rt_multi_create(const int32_t* devices, int32_t nlocal, int32_t nranks, int3
             if (e == hipSuccess) e = hipEventCreateWithFlags(&k->ev_sent[s], hipEventDisableTiming);
             // recorded once, so the first wait on a slot (no send yet) is already satisfied
             if (e == hipSuccess) e = hipEventRecord(k->ev_sent[s], k->comm_stream);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&k->ev_ready[s], hipEventDisableTiming);
         }
         if (e == hipSuccess) e = hipEventCreateWithFlags(&k->ev_done, hipEventDisableTiming);
         if (e != hipSuccess) fail(hip_err(m, e, "rank streams/events"));
@@ -594,10 +758,20 @@ int rt_multi_create(const int32_t* devices, int32_t nlocal, int32_t nranks, int3
             }
         }
     }
+    if (st == RT_OK && m->threads()) {
+        // the mailbox of this unique id, shared with the other ranks' handles
+        m->hub_key.assign(reinterpret_cast<const char*>(unique_id), RT_MULTI_ID_BYTES);
+        std::lock_guard<std::mutex> lk(g_hubs_mu);
+        auto& h = g_hubs[m->hub_key];
+        if (!h) h = std::make_shared<Hub>();
+        m->hub = h;
+        std::lock_guard<std::mutex> lk2(h->mu);
+        h->refs++;
+    }
     // one rank: the band is the frame and nothing is exchanged, so no communicator (RCCL's
     // init would only print its banner on stdout and start its proxy thread) — except for
     // the loopback transport, whose root sends its band to itself
-    if (st == RT_OK && m->gathers()) {
+    if (st == RT_OK && m->gathers() && m->rccl()) {
         ncclUniqueId id;
         if (one_process && !unique_id) {
             if (ncclGetUniqueId(&id) != ncclSuccess) fail(nccl_err(m, ncclInternalError, "ncclGetUniqueId"));
@@ -655,6 +829,18 @@ int rt_multi_destroy(rt_multi* m) {
     if (m->broken) abort_comms(m);
     for (Rank* k : m->r) destroy_rank(k, m->broken);
     m->r.clear();
+    if (m->hub) {
+        // peers still waiting on this handle give up; the last handle drops the mailbox
+        hub_fail(m);
+        std::lock_guard<std::mutex> lk(g_hubs_mu);
+        bool last;
+        {
+            std::lock_guard<std::mutex> lk2(m->hub->mu);
+            last = --m->hub->refs == 0;
+        }
+        if (last) g_hubs.erase(m->hub_key);
+        m->hub.reset();
+    }
     // the root's device objects (every rank has been synchronised above)
     for (auto& e : m->ev_in)
         if (e) (void)hipEventDestroy(e);
@@ -678,8 +864,7 @@ int rt_multi_set_scene(rt_multi* m, const rt_prim* prims, int32_t n) {
 int rt_multi_set_option(rt_multi* m, int32_t option, int64_t value) {
     if (!m) return RT_ERR_INVALID_ARG;
     if (option == RT_OPT_MULTI_LAYOUT) {
-        if (value != 0 && value != 1) return RT_ERR_INVALID_ARG;
-        if (value == 1 && rt_tile_rows() != 8) return RT_ERR_UNSUPPORTED;  // parts of 8-row tile rows
+        if (value < 0 || value > 2) return RT_ERR_INVALID_ARG;
         const int st = rt_multi_sync(m);  // frames in flight keep the layout they started with
         if (st != RT_OK) return st;
         m->layout = (int)value;
@@ -689,6 +874,51 @@ int rt_multi_set_option(rt_multi* m, int32_t option, int64_t value) {
         const int st = rt_set_option(k->ctx, option, value);
         if (st != RT_OK) return ctx_err(m, k, st, "rt_set_option");
     }
+    return RT_OK;
+}
+
+int rt_multi_set_row_weights(rt_multi* m, const float* weights, int32_t n) {
+    if (!m || n < 0 || (n > 0 && !weights)) return RT_ERR_INVALID_ARG;
+    for (int32_t t = 0; t < n; t++)
+        if (!(weights[t] >= 0.0f) || weights[t] > 3.0e38f) return RT_ERR_INVALID_ARG;
+    const int st = rt_multi_sync(m);  // frames in flight keep the bands they started with
+    if (st != RT_OK) return st;
+    m->weights.assign(weights, weights + n);
+    return RT_OK;
+}
+
+int rt_weighted_band_rows(int32_t height, int32_t nranks, int32_t rank, const float* weights,
+                          int32_t n, int32_t* row0, int32_t* nrows) {
+    if (!row0 || !nrows || height < 0 || nranks <= 0 || rank < 0 || rank >= nranks || n < 0)
+        return RT_ERR_INVALID_ARG;
+    const int32_t TH = rt_tile_rows(), T = (height + TH - 1) / TH;
+    if (n != T || (n > 0 && !weights)) return RT_ERR_INVALID_ARG;
+    // prefix sums in double, in a fixed order: every rank computes the same boundaries
+    std::vector<double> P((size_t)T + 1, 0.0);
+    for (int32_t t = 0; t < T; t++) {
+        if (!(weights[t] >= 0.0f)) return RT_ERR_INVALID_ARG;
+        P[t + 1] = P[t] + (double)weights[t];
+    }
+    const double total = P[T];
+    auto boundary = [&](int32_t r) -> int32_t {  // tile row where band r starts
+        if (r <= 0) return 0;
+        if (r >= nranks) return T;
+        if (!(total > 0.0)) return (int32_t)(((int64_t)T * r) / nranks);  // no weight: equal tile rows
+        const double target = total * r / nranks;
+        // first t with P[t] >= target, then the nearer of t - 1 and t (ties: the lower)
+        int32_t t = (int32_t)(std::lower_bound(P.begin(), P.end(), target) - P.begin());
+        if (t > T) t = T;
+        if (t > 0 && target - P[t - 1] <= P[t] - target) t--;
+        return t;
+    };
+    int32_t b0 = 0, b1 = 0;
+    for (int32_t r = 1; r <= rank + 1; r++) {  // non-decreasing boundaries
+        const int32_t b = std::max(b1, boundary(r));
+        b0 = b1;
+        b1 = b;
+    }
+    *row0 = std::min(height, b0 * TH);
+    *nrows = std::min(height, b1 * TH) - *row0;
     return RT_OK;
 }
 

@@ -169,6 +169,12 @@ __device__ unsigned long long g_diag[16];
 #ifndef RT_STACK_LDS      // 1: the cull kernels keep the recursion stack in LDS (trace_pixel_d)
 #define RT_STACK_LDS 1
 #endif
+/* RT_AB_SLIM (A/B builds only, tools/build_variant.sh): instantiate the PATH64 no-sun
+ * kernels of depth <= 8 alone (c1-c5's bench kernels), so an experiment compiles in a
+ * fraction of the full family's time; any other launch fails with hipErrorInvalidValue. */
+#ifndef RT_AB_SLIM
+#define RT_AB_SLIM 0
+#endif
 #ifndef RT_F32_READLANE   // F32 survivor records: 1 = v_readlane from the culling lane,
 #define RT_F32_READLANE 0 // 0 = scalar loads (A/B: c5 -13%); fp64 paths keep v_readlane
 #endif
@@ -2632,7 +2638,7 @@ k_trace(KParams p) {
 #ifndef RT_WPE_PAIR
 #define RT_WPE_PAIR 3
 #endif
-#if RT_WAVES_PER_BLOCK == 1 && !RT_TILE_PAIRS  // one-wave 8x8 tiles only (see launch_trace_ns)
+#if RT_WAVES_PER_BLOCK == 1 && !RT_TILE_PAIRS && !RT_AB_SLIM  // one-wave 8x8 tiles only (see launch_trace_ns)
 template <bool SUN, int MAXD>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RT_WPE_PAIR, 8)))
 k_trace_pair(KParams p) {
@@ -2692,15 +2698,27 @@ static void launch_one(const KParams& p, dim3 grid, hipStream_t st, hipEvent_t d
 }
 template <int PREC, bool SUN, bool INT_EXP, bool CULL>
 static hipError_t launch_depth(const KParams& p, dim3 grid, hipStream_t st, hipEvent_t done) {
-    if (p.depth <= MAXD_SMALL)
-        launch_one<PREC, SUN, INT_EXP, CULL, MAXD_SMALL>(p, grid, st, done);
-    else if (p.depth <= MAXD_MID)
-        launch_one<PREC, SUN, INT_EXP, CULL, MAXD_MID>(p, grid, st, done);
-    else if (p.depth <= MAXD_REF)
-        launch_one<PREC, SUN, INT_EXP, CULL, MAXD_REF>(p, grid, st, done);
-    else
-        launch_one<PREC, SUN, INT_EXP, CULL, MAXD_LARGE>(p, grid, st, done);
-    return hipGetLastError();
+    if constexpr (RT_AB_SLIM && (PREC != PREC_PATH64 || SUN)) {
+        return hipErrorInvalidValue;
+    } else if constexpr (RT_AB_SLIM) {
+        if (p.depth <= MAXD_SMALL)
+            launch_one<PREC, SUN, INT_EXP, CULL, MAXD_SMALL>(p, grid, st, done);
+        else if (p.depth <= MAXD_MID)
+            launch_one<PREC, SUN, INT_EXP, CULL, MAXD_MID>(p, grid, st, done);
+        else
+            return hipErrorInvalidValue;
+        return hipGetLastError();
+    } else {
+        if (p.depth <= MAXD_SMALL)
+            launch_one<PREC, SUN, INT_EXP, CULL, MAXD_SMALL>(p, grid, st, done);
+        else if (p.depth <= MAXD_MID)
+            launch_one<PREC, SUN, INT_EXP, CULL, MAXD_MID>(p, grid, st, done);
+        else if (p.depth <= MAXD_REF)
+            launch_one<PREC, SUN, INT_EXP, CULL, MAXD_REF>(p, grid, st, done);
+        else
+            launch_one<PREC, SUN, INT_EXP, CULL, MAXD_LARGE>(p, grid, st, done);
+        return hipGetLastError();
+    }
 }
 template <int PREC, bool SUN, bool INT_EXP>
 static hipError_t launch_cull(const KParams& p, dim3 grid, hipStream_t st, hipEvent_t done) {
@@ -2742,7 +2760,7 @@ int launch_trace_ns(const KParams& p, int prec, void* stream, void* done_event) 
     hipEvent_t done = static_cast<hipEvent_t>(done_event);
     // two pixels per lane exist only in one-wave (8x8 tile) builds: the pair kernel is not
     // instantiated for RT_WAVES_PER_BLOCK > 1 or RT_TILE_PAIRS (RT_OPT_PIXEL_PAIRS ignored)
-#if RT_WAVES_PER_BLOCK == 1 && !RT_TILE_PAIRS
+#if RT_WAVES_PER_BLOCK == 1 && !RT_TILE_PAIRS && !RT_AB_SLIM
     if (p.pairs && prec == PREC_PATH64 && !p.wave_cull) {
         // 16x8 pixels per wave: half the tile columns per dispatch unit
         const int gxp = (((p.W + TILE_W - 1) / TILE_W) + 1) >> 1;

@@ -32,6 +32,7 @@ RT_ERR_COMM = 8
 RT_TRANSPORT_RCCL = 0
 RT_TRANSPORT_COPY = 1
 RT_TRANSPORT_RCCL_LOOPBACK = 2
+RT_TRANSPORT_THREADS = 3   # rehearsal: one handle per rank in one process (include/rt_capi.h)
 RT_MULTI_ID_BYTES = 128
 RT_MULTI_SLOTS = 2
 
@@ -164,6 +165,13 @@ SIGNATURES = [
      [C.c_void_p, C.POINTER(rt_camera), C.c_int32, C.c_int32, C.c_uint32, C.c_int32, C.c_void_p,
       C.POINTER(rt_stats)]),
     ("rt_multi_sync", C.c_int, [C.c_void_p]),
+    ("rt_multi_set_row_weights", C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.c_int32]),
+    ("rt_weighted_band_rows", C.c_int,
+     [C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_float), C.c_int32, C.POINTER(C.c_int32),
+      C.POINTER(C.c_int32)]),
+    ("rt_tile_row_costs", C.c_int,
+     [C.c_void_p, C.POINTER(rt_camera), C.c_int32, C.c_int32, C.c_uint32, C.POINTER(C.c_float),
+      C.c_int32]),
 ]
 
 _lib = None
@@ -246,6 +254,23 @@ def band_rows(height: int, nranks: int, rank: int) -> tuple[int, int]:
     lib = load()
     r0, nr = C.c_int32(), C.c_int32()
     check(lib.rt_band_rows(height, nranks, rank, C.byref(r0), C.byref(nr)))
+    return r0.value, nr.value
+
+
+def tile_rows_of(height: int) -> int:
+    """Tile rows of a frame of `height` pixel rows (rt_tile_rows() rows each)."""
+    th = load().rt_tile_rows()
+    return (height + th - 1) // th
+
+
+def weighted_band_rows(height: int, nranks: int, rank: int, weights) -> tuple[int, int]:
+    """rt_weighted_band_rows: contiguous band of `rank` cut at tile rows so every band
+    carries ~1/nranks of the per-tile-row weights."""
+    lib = load()
+    w = list(weights)
+    arr = (C.c_float * max(1, len(w)))(*w)
+    r0, nr = C.c_int32(), C.c_int32()
+    check(lib.rt_weighted_band_rows(height, nranks, rank, arr, len(w), C.byref(r0), C.byref(nr)))
     return r0.value, nr.value
 
 
@@ -349,6 +374,16 @@ class Renderer:
                                         C.c_void_p(d_segments or None),
                                         C.c_void_p(stream or None)), self.ctx)
 
+    def tile_row_costs(self, cam: rt_camera, depth: int, precision: int = RT_PREC_PATH64,
+                       flags: int = 0):
+        """rt_tile_row_costs: measured cost (sum of the waves' shader cycles / 32) of every
+        tile row of one render of the whole frame (synchronous) -> numpy float32."""
+        n = tile_rows_of(cam.height)
+        out = np.zeros(max(1, n), np.float32)
+        check(self.lib.rt_tile_row_costs(self.ctx, C.byref(cam), depth, precision, flags,
+                                         out.ctypes.data_as(C.POINTER(C.c_float)), n), self.ctx)
+        return out[:n]
+
     def render_device_interleaved(self, cam: rt_camera, depth: int, nparts: int, part: int,
                                   d_out: int, precision: int = RT_PREC_F64, flags: int = 0,
                                   out_format: int = RT_OUT_RGB_F32, out_frame_rows: bool = False,
@@ -392,6 +427,8 @@ class MultiRenderer:
     MultiRenderer([0, 1, 2, 3])                         one process drives 4 GPUs (RCCL)
     MultiRenderer([0, 0, 0], transport=RT_TRANSPORT_COPY)  3 ranks on one GPU, peer copies
     MultiRenderer([local], nranks=N, first_rank=rank, unique_id=id)   one process per GPU
+    MultiRenderer([0], nranks=N, first_rank=r, unique_id=id, transport=RT_TRANSPORT_THREADS)
+        rank r of N handles in this process, each driven from its own thread (rehearsal)
     """
 
     def __init__(self, devices, nranks: int | None = None, first_rank: int = 0,
@@ -477,3 +514,10 @@ class MultiRenderer:
 
     def sync(self) -> None:
         self._check(self.lib.rt_multi_sync(self.m))
+
+    def set_row_weights(self, weights) -> None:
+        """rt_multi_set_row_weights: per-tile-row weights of RT_OPT_MULTI_LAYOUT = 2 (the
+        same on every rank; None or [] clears them)."""
+        w = [float(x) for x in (weights if weights is not None else [])]
+        arr = (C.c_float * max(1, len(w)))(*w)
+        self._check(self.lib.rt_multi_set_row_weights(self.m, arr, len(w)))

@@ -131,7 +131,14 @@ def test_multi_args_rejected_without_device():
     # processes; an unknown transport is rejected
     assert lib.rt_multi_create(devs, 1, 2, 1, None, capi.RT_TRANSPORT_RCCL_LOOPBACK,
                                C.byref(h)) == capi.RT_ERR_INVALID_ARG
-    assert lib.rt_multi_create(devs, 1, 2, 0, None, 3, C.byref(h)) == capi.RT_ERR_INVALID_ARG
+    assert lib.rt_multi_create(devs, 1, 2, 0, None, 9, C.byref(h)) == capi.RT_ERR_INVALID_ARG
+    # THREADS (the in-process rehearsal of one process per GPU): one rank per handle, at least
+    # two ranks, the shared id that keys its mailbox
+    th = capi.RT_TRANSPORT_THREADS
+    assert lib.rt_multi_create(devs, 1, 2, 0, None, th, C.byref(h)) == capi.RT_ERR_INVALID_ARG
+    assert lib.rt_multi_create(devs, 2, 2, 0, uid, th, C.byref(h)) == capi.RT_ERR_INVALID_ARG
+    assert lib.rt_multi_create(devs, 1, 1, 0, uid, th, C.byref(h)) == capi.RT_ERR_INVALID_ARG
+    assert lib.rt_multi_set_row_weights(None, None, 0) == capi.RT_ERR_INVALID_ARG
     if not has_gpu():
         assert lib.rt_multi_create(devs, 1, 1, 0, None, 0, C.byref(h)) == capi.RT_ERR_NO_DEVICE
     assert lib.rt_multi_destroy(None) == capi.RT_ERR_INVALID_ARG
@@ -169,3 +176,46 @@ def test_interleaved_rows_partition():
             assert max(sizes) - min(sizes) <= 8
     with pytest.raises(capi.RTError):
         capi.interleaved_rows(10, 2, 2)
+
+
+def test_weighted_band_rows_partition_and_balance():
+    """rt_weighted_band_rows (RT_OPT_MULTI_LAYOUT = 2): contiguous bands whose boundaries fall
+    on tile rows, covering every frame row once, each boundary the tile row whose weight prefix
+    is nearest r/N of the total — so the heaviest band carries at most 1/N of the weight plus
+    one tile row's; equal weights give equal tile rows; no weight at all gives equal tile rows
+    too; every rank computes the same boundaries from the same weights."""
+    rng = np.random.default_rng(7)
+    for h in (1, 7, 8, 9, 36, 1080, 4320):
+        T = capi.tile_rows_of(h)
+        for n in (1, 2, 3, 4, 8):
+            for kind in ("rand", "peak", "equal", "zero"):
+                if kind == "rand":
+                    w = rng.random(T).astype(np.float32)
+                elif kind == "peak":
+                    w = np.exp(-((np.arange(T) - 0.6 * T) / max(1.0, 0.05 * T)) ** 2).astype(np.float32)
+                elif kind == "equal":
+                    w = np.ones(T, np.float32)
+                else:
+                    w = np.zeros(T, np.float32)
+                rows, bands = [], []
+                for r in range(n):
+                    r0, nr = capi.weighted_band_rows(h, n, r, w)
+                    assert nr >= 0
+                    assert r0 % 8 == 0 or nr == 0 or r0 == h
+                    rows.extend(range(r0, r0 + nr))
+                    bands.append((r0, nr))
+                assert rows == list(range(h)), (h, n, kind)
+                tot = float(np.sum(w, dtype=np.float64))
+                if kind in ("rand", "peak") and tot > 0:
+                    for r0, nr in bands:
+                        t0, t1 = r0 // 8, (r0 + nr + 7) // 8
+                        assert float(np.sum(w[t0:t1], dtype=np.float64)) <= tot / n + 2 * float(w.max()) + 1e-6
+                if kind in ("equal", "zero") and T >= n:
+                    tiles = [(r0 + nr + 7) // 8 - r0 // 8 for r0, nr in bands]
+                    assert max(tiles) - min(tiles) <= 1, (h, n, kind, tiles)
+    with pytest.raises(capi.RTError):
+        capi.weighted_band_rows(1080, 2, 0, [1.0] * 10)          # not one weight per tile row
+    with pytest.raises(capi.RTError):
+        capi.weighted_band_rows(16, 2, 0, [1.0, float("nan")])   # weights must be >= 0
+    with pytest.raises(capi.RTError):
+        capi.weighted_band_rows(16, 2, 2, [1.0, 1.0])            # rank past nranks

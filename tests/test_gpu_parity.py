@@ -821,7 +821,7 @@ def test_render_device_frames_equals_per_frame_calls(rend):
 
 def test_row_feedback_isolated_sampling_in_flight(rend):
     """Row feedback on frames in flight (three caller streams, a snapshot every other
-    frame): with RT_OPT_ROW_FEEDBACK_ISOLATE on (default) the sampled frames are ordered
+    frame): with RT_OPT_ROW_FEEDBACK_ISOLATE on (default off) the sampled frames are ordered
     between their neighbours on the device, and every frame is still the same frame —
     each buffer bitwise equal to a plain render, isolation on or off, for a full frame and
     a ragged band (the snapshot's per-unit reduction k_unit_max covers both)."""
@@ -848,7 +848,7 @@ def test_row_feedback_isolated_sampling_in_flight(rend):
         with pytest.raises(capi.RTError):
             rend.set_option(capi.RT_OPT_ROW_FEEDBACK_ISOLATE, 2)
     finally:
-        rend.set_option(capi.RT_OPT_ROW_FEEDBACK_ISOLATE, 1)
+        rend.set_option(capi.RT_OPT_ROW_FEEDBACK_ISOLATE, 0)   # the product default
         rend.set_option(capi.RT_OPT_ROW_FEEDBACK, 32)
 
 

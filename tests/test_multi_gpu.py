@@ -254,14 +254,15 @@ def test_multi_interleaved_layout_bitwise(rend, n):
             for b in bufs:
                 assert np.array_equal(b.cpu().numpy().view(np.uint32), ref.view(np.uint32)), (n, w)
         with pytest.raises(capi.RTError):
-            m.set_option(capi.RT_OPT_MULTI_LAYOUT, 2)
+            m.set_option(capi.RT_OPT_MULTI_LAYOUT, 3)
 
 
-def test_loopback_rccl_c4_full_size_and_interleaved_frames(rend):
+def test_loopback_rccl_c4_full_size_frames_in_flight(rend):
     """RT_TRANSPORT_RCCL_LOOPBACK at config 4's full size: PATH64 fp32 RGB, RGBA8 and F64
     frames through RCCL send/recv (root to itself) bitwise the one-GPU frame, then 9 frames
-    in flight on two caller streams (the root's band slots reused while its self-sends are
-    pending), every frame complete on its stream; rt_multi_sync checks RCCL's async error."""
+    in flight alternating over two caller streams (the root's band slots reused while its
+    self-sends are pending), every frame complete on its stream; rt_multi_sync checks RCCL's
+    async error."""
     import torch
     dev = torch.device("cuda", 0)
     cfg = scenes.CONFIGS["c2"]
@@ -288,26 +289,162 @@ def test_loopback_rccl_c4_full_size_and_interleaved_frames(rend):
             assert np.array_equal(b.cpu().numpy().view(np.uint32), ref.view(np.uint32))
 
 
-def test_failed_frame_breaks_the_communicator(rend):
-    """A frame that fails after the gather may have been queued (here: no scene on the
-    ranks yet) leaves the communicator out of step: the rt_multi reports RT_ERR_COMM on
-    every later frame and on rt_multi_sync (which aborts the communicator instead of
-    waiting), and destroying it returns (ncclCommAbort, no hang)."""
+def test_failure_before_the_gather_is_queued_keeps_the_communicator(rend):
+    """A frame that fails before any rank queued its part of the gather (here: no scene
+    yet, rejected before the root's loopback send/recv) returns its own status and leaves
+    the RCCL communicator usable: the next frame, once the scene is set, is bitwise the
+    one-GPU frame (a caller probing options must not brick the object)."""
     import torch
     dev = torch.device("cuda", 0)
     cam = _cam(64, 36)
     buf = torch.zeros((36, 64, 3), device=dev)
+    prims = scenes.to_prims(scenes.synthetic_scene(8, 4))
     m = capi.MultiRenderer([0], transport=capi.RT_TRANSPORT_RCCL_LOOPBACK)
     try:
         with pytest.raises(capi.RTError) as e1:
             m.render_device(cam, 2, buf.data_ptr(), capi.RT_PREC_PATH64)
         assert e1.value.status == capi.RT_ERR_NO_SCENE
-        m.set_scene(scenes.to_prims(scenes.synthetic_scene(8, 4)))
-        with pytest.raises(capi.RTError) as e2:
-            m.render_device(cam, 2, buf.data_ptr(), capi.RT_PREC_PATH64)
-        assert e2.value.status == capi.RT_ERR_COMM
-        with pytest.raises(capi.RTError) as e3:
-            m.sync()
-        assert e3.value.status == capi.RT_ERR_COMM
+        m.set_scene(prims)
+        m.render_device(cam, 2, buf.data_ptr(), capi.RT_PREC_PATH64)
+        torch.cuda.synchronize()
+        m.sync()
+        rend.set_scene(prims)
+        ref, _ = rend.render(cam, 2, capi.RT_PREC_PATH64)
+        assert np.array_equal(buf.cpu().numpy().view(np.uint32), ref.view(np.uint32))
     finally:
         m.close()
+
+
+def _run_threads(handles, fn):
+    """Drive every THREADS handle from its own thread (as one process per GPU would) and
+    return the per-rank exceptions (None = ok)."""
+    import threading
+    errs = [None] * len(handles)
+
+    def body(r):
+        try:
+            fn(r, handles[r])
+        except BaseException as e:   # noqa: BLE001 - reported by the caller
+            errs[r] = e
+
+    ths = [threading.Thread(target=body, args=(r,)) for r in range(len(handles))]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(120)
+        assert not t.is_alive(), "a THREADS rank hung"
+    return errs
+
+
+@pytest.mark.parametrize("n,layout", [(2, 0), (3, 1), (8, 1), (4, 2), (8, 2)])
+def test_threads_transport_runs_the_process_per_gpu_branches(rend, n, layout):
+    """RT_TRANSPORT_THREADS: n rt_multi handles in this process, one per rank (nlocal = 1,
+    first_rank = r, one shared id), each driven from its own thread exactly as the
+    process-per-GPU bench drives its rank — so the branches the first multi-GPU run takes
+    execute here on one GPU: the non-root ranks without a frame buffer (nbufs = 0) rendering
+    into their band slots and "sending" (a peer copy matched through the mailbox instead of
+    ncclSend), their caller streams waiting on the send (ev_sent), and the root receiving
+    every part — contiguous bands straight into the frame rows (layout 0), interleaved parts
+    into its staging buffers then scattered by strided copies (layout 1: the staging
+    allocation, slot reuse and scatter of the RCCL path), cost-weighted bands (layout 2).
+    Config 4's full frame (1920x1080, c2 scene, depth 4), 7 frames of a moving camera in
+    flight over two root buffers: every buffer is bitwise the one-GPU frame of the last camera
+    written to it, and a rank's band is already in the root's frame when its caller stream
+    has passed the frame (checked on the last frame)."""
+    import os
+    import torch
+    dev = torch.device("cuda", 0)
+    cfg = scenes.CONFIGS["c2"]
+    prims = scenes.to_prims(cfg.scene())
+    rend.set_scene(prims)
+    W, H = cfg.width, cfg.height
+    cams = [_cam(W, H, 0.02 * k) for k in range(5)]
+    refs = [rend.render(c, 4, capi.RT_PREC_PATH64, 0, capi.RT_OUT_RGB_F32)[0] for c in cams]
+    weights = rend.tile_row_costs(cams[0], 4, capi.RT_PREC_PATH64) if layout == 2 else None
+    uid = os.urandom(capi.RT_MULTI_ID_BYTES)
+    hs = [capi.MultiRenderer([0], nranks=n, first_rank=r, unique_id=uid,
+                             transport=capi.RT_TRANSPORT_THREADS) for r in range(n)]
+    bufs = [torch.full((H, W, 3), -1.0, dtype=torch.float32, device=dev) for _ in range(2)]
+    root_sts = [torch.cuda.Stream(dev) for _ in range(2)]
+    rank_sts = [torch.cuda.Stream(dev) for _ in range(n)]
+    nf = 7
+    last = nf - 1
+    snaps = [None] * n
+    try:
+        for h in hs:
+            h.set_scene(prims)
+            h.set_option(capi.RT_OPT_MULTI_LAYOUT, layout)
+            if weights is not None:
+                h.set_row_weights(weights)
+        torch.cuda.synchronize()
+
+        def drive(r, h):
+            if r == 0:
+                h.render_device_frames(cams, 4, [b.data_ptr() for b in bufs],
+                                       streams=[s.cuda_stream for s in root_sts], nframes=nf)
+                return
+            h.render_device_frames(cams, 4, [], streams=[rank_sts[r].cuda_stream], nframes=nf)
+            # past this point on the caller's stream, the rank's last band has landed in the
+            # root's frame (rt_multi_render_device: "a non-NULL stream ... waits for the rank's
+            # band to have been sent")
+            ev = torch.cuda.Event()
+            ev.record(rank_sts[r])
+            ev.synchronize()
+            snaps[r] = bufs[last % 2].cpu().numpy()
+
+        errs = _run_threads(hs, drive)
+        assert errs == [None] * n, errs
+        torch.cuda.synchronize()
+        for h in hs:
+            h.sync()
+        for b in range(2):
+            lf = max(f for f in range(nf) if f % 2 == b)
+            got = bufs[b].cpu().numpy()
+            assert np.array_equal(got.view(np.uint32), refs[lf % len(cams)].view(np.uint32)), (n, layout, b)
+        ref_last = refs[last % len(cams)]
+        for r in range(1, n):
+            if layout == 1:
+                rows = capi.interleaved_row_index(H, n, r)
+            elif layout == 2:
+                r0, nr = capi.weighted_band_rows(H, n, r, weights)
+                rows = list(range(r0, r0 + nr))
+            else:
+                r0, nr = capi.band_rows(H, n, r)
+                rows = list(range(r0, r0 + nr))
+            assert np.array_equal(snaps[r][rows].view(np.uint32), ref_last[rows].view(np.uint32)), (n, layout, r)
+    finally:
+        for h in hs:
+            h.close()
+
+
+def test_threads_transport_a_failed_rank_ends_the_exchange(rend):
+    """A rank whose frame fails (no scene on that rank only) ends the exchange for every
+    handle: the root, already waiting for that rank's part, returns RT_ERR_COMM instead of
+    hanging; both handles are broken (later frames and rt_multi_sync: RT_ERR_COMM) and close
+    cleanly."""
+    import os
+    import torch
+    dev = torch.device("cuda", 0)
+    cam = _cam(160, 90)
+    uid = os.urandom(capi.RT_MULTI_ID_BYTES)
+    hs = [capi.MultiRenderer([0], nranks=2, first_rank=r, unique_id=uid,
+                             transport=capi.RT_TRANSPORT_THREADS) for r in range(2)]
+    buf = torch.zeros((90, 160, 3), device=dev)
+    st = torch.cuda.Stream(dev)
+    try:
+        hs[0].set_scene(scenes.to_prims(scenes.synthetic_scene(8, 4)))
+
+        def drive(r, h):
+            h.render_device(cam, 2, buf.data_ptr() if r == 0 else 0, capi.RT_PREC_PATH64,
+                            stream=st.cuda_stream if r else 0)
+
+        errs = _run_threads(hs, drive)
+        assert isinstance(errs[0], capi.RTError) and errs[0].status == capi.RT_ERR_COMM, errs
+        assert isinstance(errs[1], capi.RTError) and errs[1].status == capi.RT_ERR_NO_SCENE, errs
+        for h in hs:
+            with pytest.raises(capi.RTError) as e:
+                h.sync()
+            assert e.value.status == capi.RT_ERR_COMM
+    finally:
+        for h in hs:
+            h.close()

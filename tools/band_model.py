@@ -19,10 +19,12 @@ sys.path.insert(0, os.path.join(REPO, "ray-tracer-from-scratch_amd"))
 from rtamd import capi, scenes  # noqa: E402
 
 
-def pipelined_us(torch, st, st2, launch_on, n, extra=()):
+def pipelined_us(torch, st, st2, launch_on, n, extra=(), frames=None):
     """Per-frame GPU time of n frames round-robin over 2 + len(extra) streams (frames in
     flight: one frame's tail overlaps the next ones' start, as in bench.py's frame loop).
-    A first untimed pass warms every stream (its first launch carries one-time costs)."""
+    A first untimed pass warms every stream (its first launch carries one-time costs).
+    frames(streams, m): enqueue m frames by one C-ABI call (rt_render_device_frames, as a
+    rank's frame loop does: no Python between frames); else launch_on(stream, buf) per frame."""
     sts = [st, st2] + list(extra)
     for timed in (False, True):
         torch.cuda.synchronize()
@@ -31,7 +33,9 @@ def pipelined_us(torch, st, st2, launch_on, n, extra=()):
         for s_ in sts[1:]:
             s_.wait_stream(st)
         m = n if timed else len(sts)
-        for k in range(m):
+        if frames is not None:
+            frames(sts, m)
+        for k in range(m if frames is None else 0):
             launch_on(sts[k % len(sts)], k % 2)
         for s_ in sts[1:]:
             st.wait_stream(s_)
@@ -87,7 +91,9 @@ def main():
     ap.add_argument("--precision", default="path64")
     ap.add_argument("--launches", type=int, default=100)
     ap.add_argument("--splits", default="1,2,4,8")
-    ap.add_argument("--layout", choices=("contiguous", "interleaved"), default="contiguous")
+    ap.add_argument("--layout", choices=("contiguous", "interleaved", "weighted"), default="contiguous",
+                    help="weighted: contiguous bands cut by rt_weighted_band_rows over the "
+                         "measured tile-row costs of one full-frame render (rt_tile_row_costs)")
     args = ap.parse_args()
     import torch
     dev = torch.device("cuda", 0)
@@ -106,6 +112,13 @@ def main():
     res = {"config": args.config, "precision": args.precision, "width": W, "height": H,
            "layout": args.layout, "splits": {}}
     inter = args.layout == "interleaved"
+    weights = None
+    if args.layout == "weighted":
+        wr = capi.Renderer(0)
+        wr.set_scene(prims)
+        weights = wr.tile_row_costs(cam, cfg.depth, prec)
+        wr.close()
+        res["weights"] = [round(float(x), 1) for x in weights]
     for N in [int(x) for x in args.splits.split(",")]:
         bands = []
         for r in range(N):
@@ -113,7 +126,8 @@ def main():
                 bands.append(interleaved_part(capi, torch, st, cam, cfg.depth, prec, prims, out,
                                               segs, N, r, n, st2, out2, extra))
                 continue
-            r0, nr = capi.band_rows(H, N, r)
+            r0, nr = (capi.weighted_band_rows(H, N, r, weights) if weights is not None
+                      else capi.band_rows(H, N, r))
             rend = capi.Renderer(0)
             rend.set_scene(prims)
             for _ in range(40):   # warm: the measured row order for this band settles
@@ -140,8 +154,11 @@ def main():
             torch.cuda.synchronize()
             lo = lambda s_, b: rend.render_device(cam, cfg.depth, (out, out2)[b].data_ptr(), prec,
                                                   row0=r0, nrows=nr, stream=s_.cuda_stream)
-            fif2 = pipelined_us(torch, st, st2, lo, n)
-            fif4 = pipelined_us(torch, st, st2, lo, n, extra)
+            fr = lambda sts_, m: rend.render_device_frames(
+                [cam], cfg.depth, [out.data_ptr(), out2.data_ptr()], prec, row0=r0, nrows=nr,
+                streams=[x.cuda_stream for x in sts_], nframes=m)
+            fif2 = pipelined_us(torch, st, st2, lo, n, frames=fr)
+            fif4 = pipelined_us(torch, st, st2, lo, n, extra, frames=fr)
             rend.close()
             bands.append({"rank": r, "row0": r0, "nrows": nr, "kernel_us": round(kms * 1e3, 2),
                           "kernel_us_fif2": fif2, "kernel_us_fif4": fif4,
