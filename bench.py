@@ -163,6 +163,12 @@ def main() -> int:
                     help="rehearsal only (one process): split the frame over this many ranks "
                          "on this one GPU with the peer-copy transport; not a measurement")
     ap.add_argument("--sun", action="store_true", help="build-defined sun term (off = parity)")
+    ap.add_argument("--steady-frames", type=int, default=200,
+                    help="frames of the steady-state loop run right before the warmup and timed "
+                         "region (a side measurement; it also leaves the row order settled)")
+    ap.add_argument("--windows", type=int, default=40,
+                    help="windows of --steps frames run right before the warmup, each like the "
+                         "timed region (their ms/frame distribution is reported)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c5", action="store_true",
@@ -386,6 +392,24 @@ def main() -> int:
         for s_ in streams[1:]:
             stream.wait_stream(s_)
 
+    sync_evs = [torch.cuda.Event() for _ in range(len(streams) + 1)]
+
+    hs_t = [0.0, 0.0]
+
+    def hot_sync():
+        """torch.cuda.synchronize, reached by polling events on this rank's streams first: a
+        host core that sleeps in a blocking wait clocks down, and the frames enqueued right
+        after took 19-24 us of host time each instead of 9-10 (measured) —
+        slower than the GPU renders them, so the GPU starved in the next timed window."""
+        for e_, s_ in zip(sync_evs, streams + [torch.cuda.current_stream(dev)]):
+            e_.record(s_)
+        for e_ in sync_evs:
+            while not e_.query():
+                pass
+        hs_t[0] = time.perf_counter()
+        torch.cuda.synchronize(dev)
+        hs_t[1] = time.perf_counter()
+
     def timed_frames(cams, nframes, fl, nrep=2):
         """Best ms/frame of nframes frames of `cams` (cycled) through the frames-in-flight
         loop on this rank's rows (HIP events on stream 0, every stream joined)."""
@@ -476,7 +500,7 @@ def main() -> int:
     # regions 33-40 us/frame vs 29 over 200 frames) ----
     steady = None
     if not args.no_sweep:
-        nst = 200
+        nst = max(1, args.steady_frames)
         torch.cuda.synchronize(dev)
         if multi is not None:
             multi.sync()
@@ -490,7 +514,7 @@ def main() -> int:
         run_steps(nst)
         join_streams()
         es1.record(stream)
-        torch.cuda.synchronize(dev)
+        hot_sync()
         if multi is not None:
             multi.sync()
         barrier()
@@ -501,32 +525,63 @@ def main() -> int:
                   "mrays_per_s": round(total_segs * nst / float(tst.item()) / 1e6, 1),
                   "stream_ms_per_step": round(es0.elapsed_time(es1) / nst, 4)}
 
+    # ---- window rhythm: R windows exactly like the timed region (K frames by one call,
+    # bracketed by the same syncs and barrier), back to back.  Their ms/frame is the
+    # distribution the timed window is one sample of (reported), and the timed window then
+    # runs as the next window of the same rhythm: the GPU's clock governor ramps its shader
+    # clock over ~20 ms of sustained load (2.2 -> 2.4 GHz measured inside the frames) and a
+    # host core that slept clocks down ----
+    windows = None
+    if not args.no_sweep and args.windows > 0:
+        wms = []
+        for _ in range(args.windows):
+            hot_sync()
+            barrier()
+            tw0 = time.perf_counter()
+            run_steps(args.steps)
+            hot_sync()
+            barrier()
+            wms.append((time.perf_counter() - tw0) / args.steps * 1e3)
+        if multi is not None:
+            multi.sync()
+        tw = torch.tensor(wms, dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(tw, op=dist.ReduceOp.MAX)
+        q = sorted(tw.tolist())
+        windows = {"windows": len(q), "frames_per_window": args.steps,
+                   "ms_per_step_median": round(q[len(q) // 2], 4),
+                   "ms_per_step_p10": round(q[int(0.1 * (len(q) - 1))], 4),
+                   "ms_per_step_p90": round(q[int(0.9 * (len(q) - 1))], 4),
+                   "mrays_per_s_median": round(total_segs / (q[len(q) // 2] * 1e-3) / 1e6, 1)}
+
     # ---- warmup + timed region ----
     run_steps(args.warmup)
-    torch.cuda.synchronize(dev)
+    hot_sync()
     if multi is not None:
         multi.sync()
     barrier()
-    torch.cuda.synchronize(dev)
+    hot_sync()
     ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
+    ev1s = [torch.cuda.Event(enable_timing=True) for _ in streams]
     t0 = time.perf_counter()
     ev0.record(stream)
     for s_ in streams[1:]:
         s_.wait_stream(stream)
     run_steps(args.steps)
-    join_streams()
-    ev1.record(stream)
-    torch.cuda.synchronize(dev)
-    if multi is not None:
-        multi.sync()
-    barrier()
+    t_enq = time.perf_counter() - t0   # host time to enqueue the K frames (diagnostic)
+    for e_, s_ in zip(ev1s, streams):  # (while the GPU still renders: off the critical path)
+        e_.record(s_)
+    hot_sync()   # every stream of the device: the gathered frames included (N > 1, the
+    barrier()    # caller streams wait on the gather)
     t1 = time.perf_counter()
+    t_polled, t_synced = hs_t[0] - t0, hs_t[1] - t0
+    if multi is not None:
+        multi.sync()   # RCCL's asynchronous errors (after the timed region)
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     elapsed_s = float(elapsed.item())
-    stream_ms = ev0.elapsed_time(ev1) / args.steps
+    stream_ms = max(ev0.elapsed_time(e_) for e_ in ev1s) / args.steps
 
     # ---- per-launch kernel time: this rank's rows, one stream, launches back to back ----
     # (after 64 untimed frames of `rend`, whose measured row order the side loops reset)
@@ -719,6 +774,10 @@ def main() -> int:
             # back-to-back launches): the per-frame latency the rooflines are priced on
             "kernel_ms": round(kernel_ms, 4),
             "stream_ms_per_step": round(stream_ms, 4),
+            "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 4),
+            "timed_edges_us": {"polled_done": round(t_polled * 1e6, 1),
+                               "synchronized": round(t_synced * 1e6, 1),
+                               "end": round((t1 - t0) * 1e6, 1)},
             "roofline": {
                 "bound": "hbm",
                 "achieved": round(alg_bytes / kernel_s / 1e9, 2),
@@ -747,6 +806,7 @@ def main() -> int:
             "sun_extension": sun_ext,
             "moving_camera": moving,
             "steady_state": steady,
+            "window_rhythm": windows,
             "frame_sharded": sharded,
             "tiled_rgba8": tiled8,
             "c5_tiled": c5,

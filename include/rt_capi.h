@@ -208,6 +208,12 @@ enum rt_option {
                                          overlapping frames; 0 (default) = it overlaps like
                                          any frame (measured: the lost overlap costs more
                                          than cleaner costs gain).  Output is identical. */
+    RT_OPT_HOST_PIPELINE = 16,       /* 1 (default): rt_render_device_frames computes the
+                                         next frames' kernel arguments (pixel boxes, mirror
+                                         chains, eye tables) on a helper thread while the
+                                         calling thread launches the current frame; 0 = one
+                                         thread does both in turn.  The same launches in the
+                                         same order: output is identical. */
     RT_OPT_MULTI_LAYOUT = 13,        /* rt_multi_set_option only: 0 (default) = contiguous
                                          row bands (rt_band_rows); 1 = interleaved tile rows
                                          (rt_interleaved_rows): balanced when the frame's cost

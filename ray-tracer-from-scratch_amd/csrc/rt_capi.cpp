@@ -21,12 +21,16 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
+#include <condition_variable>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <functional>
 #include <memory>
+#include <mutex>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "../../include/rt_capi.h"
@@ -161,6 +165,12 @@ struct rt_ctx {
         hipEvent_t ev;
     };
     std::vector<Inflight> inflight;
+    // RT_OPT_HOST_PIPELINE: rt_render_device_frames computes frame f+1's kernel arguments
+    // (pixel boxes, mirror chains, eye tables: make_params) on a helper thread while this
+    // thread launches frame f (see render_frames_pipelined)
+    bool host_pipeline = true;
+    struct Prep;
+    Prep* prep = nullptr;
     char last_err[256] = {0};
 };
 
@@ -1124,6 +1134,10 @@ int rt_ctx_create(int device, rt_ctx** out) {
     return RT_OK;
 }
 
+namespace {
+void prep_shutdown(rt_ctx* ctx);  // RT_OPT_HOST_PIPELINE's helper thread (below)
+}
+
 int rt_ctx_destroy(rt_ctx* ctx) {
     if (!ctx) return RT_ERR_INVALID_ARG;
 #if RT_HOST_PROFILE
@@ -1133,6 +1147,7 @@ int rt_ctx_destroy(rt_ctx* ctx) {
                      g_hn - 50, g_hp[0] / m, g_hp[1] / m, g_hp[2] / m, g_hp[3] / m, g_hp[4] / m);
     }
 #endif
+    prep_shutdown(ctx);
     DeviceGuard dg(ctx->device);
     (void)wait_inflight(ctx);  // frames in flight on caller streams still read the scene
     for (auto& f : ctx->inflight) (void)hipEventDestroy(f.ev);
@@ -1249,6 +1264,10 @@ int rt_set_option(rt_ctx* ctx, int32_t option, int64_t value) {
         case RT_OPT_ROW_FEEDBACK_EMA:
             if (value < 0 || value > 95) return RT_ERR_INVALID_ARG;
             ctx->fb_ema = (int)value;
+            return RT_OK;
+        case RT_OPT_HOST_PIPELINE:
+            if (value != 0 && value != 1) return RT_ERR_INVALID_ARG;
+            ctx->host_pipeline = value == 1;
             return RT_OK;
         case RT_OPT_ROW_FEEDBACK_ISOLATE:
             if (value != 0 && value != 1) return RT_ERR_INVALID_ARG;
@@ -1463,6 +1482,73 @@ static int isolate_after(rt_ctx* ctx, hipStream_t st, bool sampled) {
     return RT_OK;
 }
 
+/* RT_OPT_HOST_PIPELINE's helper thread.  A batch (rt_render_device_frames) posts its frames;
+ * the helper computes each frame's make_params into a ring of RING slots, at most RING frames
+ * ahead of the launching thread, which takes a slot, finishes the frame (row order, launch,
+ * cost snapshot) and releases it.  make_params only reads the ctx (scene, options) and its
+ * own box cache, which no other code touches while a batch runs; everything that changes
+ * ctx state (the row feedback) stays on the launching thread. */
+struct rt_ctx::Prep {
+    static constexpr int RING = 3;
+    std::thread th;
+    std::mutex mu;
+    std::condition_variable cv;
+    bool quit = false;
+    // the posted batch (valid while gen is odd... see worker): read by the helper only
+    const rt_camera* cams = nullptr;
+    int32_t ncams = 0, row0 = 0, nrows = 0, depth = 0, precision = 0, out_format = 0, nframes = 0;
+    uint32_t flags = 0;
+    void* const* d_outs = nullptr;
+    int32_t nouts = 0;
+    std::atomic<uint64_t> posted{0}, done{0};  // batches posted / finished by the helper
+    std::atomic<int> produced{0}, consumed{0};
+    std::atomic<bool> stop{false};             // the launching thread gave up on the batch
+    rt::KParams slot[RING];
+};
+
+namespace {
+void prep_main(rt_ctx* ctx) {
+    rt_ctx::Prep& q = *ctx->prep;
+    uint64_t seen = 0;
+    for (;;) {
+        uint64_t g = q.posted.load(std::memory_order_acquire);
+        for (int it = 0; g == seen && it < 2048; it++) {
+            std::this_thread::yield();
+            g = q.posted.load(std::memory_order_acquire);
+        }
+        if (g == seen) {
+            std::unique_lock<std::mutex> lk(q.mu);
+            q.cv.wait(lk, [&] { return q.quit || q.posted.load(std::memory_order_acquire) != seen; });
+            if (q.quit) return;
+            g = q.posted.load(std::memory_order_acquire);
+        }
+        seen = g;
+        for (int f = 0; f < q.nframes; f++) {
+            while (f - q.consumed.load(std::memory_order_acquire) >= rt_ctx::Prep::RING &&
+                   !q.stop.load(std::memory_order_acquire))
+                std::this_thread::yield();
+            if (q.stop.load(std::memory_order_acquire)) break;
+            q.slot[f % rt_ctx::Prep::RING] =
+                make_params(ctx, &q.cams[f % q.ncams], q.row0, q.nrows, q.depth, q.flags, q.out_format,
+                            q.d_outs[f % q.nouts], nullptr, q.precision);
+            q.produced.store(f + 1, std::memory_order_release);
+        }
+        q.done.store(seen, std::memory_order_release);
+    }
+}
+void prep_shutdown(rt_ctx* ctx) {
+    if (!ctx->prep) return;
+    {
+        std::lock_guard<std::mutex> lk(ctx->prep->mu);
+        ctx->prep->quit = true;
+    }
+    ctx->prep->cv.notify_one();
+    if (ctx->prep->th.joinable()) ctx->prep->th.join();
+    delete ctx->prep;
+    ctx->prep = nullptr;
+}
+}  // namespace
+
 /* Pixel rows of interleaved part `part` of `nparts` (tile rows part, part + nparts, ...). */
 static int32_t interleaved_rows(int32_t height, int32_t nparts, int32_t part) {
     const int32_t T = (height + rt::TILE_H - 1) / rt::TILE_H;
@@ -1476,7 +1562,7 @@ static int32_t interleaved_rows(int32_t height, int32_t nparts, int32_t part) {
 static int render_device_impl(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nrows,
                               int32_t nparts, int32_t part, int32_t out_frame, int32_t depth,
                               int32_t precision, uint32_t flags, int32_t out_format, void* d_out,
-                              uint64_t* d_segments, void* stream) {
+                              uint64_t* d_segments, void* stream, const rt::KParams* pre = nullptr) {
 #if RT_HOST_PROFILE
     double hp_t = hp_now();
     g_hn++;
@@ -1490,9 +1576,11 @@ static int render_device_impl(rt_ctx* ctx, const rt_camera* cam, int32_t row0, i
     RT_HIP(ctx, dg.err);
     HP(0);
     // an interleaved part's tile rows span the frame: its pixel boxes are the whole frame's
-    rt::KParams p = make_params(ctx, cam, nparts > 1 ? 0 : row0, nparts > 1 ? cam->height : nrows,
-                                depth, flags, out_format, d_out,
-                                reinterpret_cast<unsigned long long*>(d_segments), precision);
+    // (pre: computed by the host pipeline's helper thread, contiguous bands only)
+    rt::KParams p = pre ? *pre
+                        : make_params(ctx, cam, nparts > 1 ? 0 : row0, nparts > 1 ? cam->height : nrows,
+                                      depth, flags, out_format, d_out,
+                                      reinterpret_cast<unsigned long long*>(d_segments), precision);
     if (nparts > 1) {
         p.row0 = 0;
         p.nrows = nrows;
@@ -1558,6 +1646,63 @@ int rt_render_device_interleaved(rt_ctx* ctx, const rt_camera* cam, int32_t npar
                               d_segments, stream);
 }
 
+/* rt_render_device_frames with the host pipeline (RT_OPT_HOST_PIPELINE): the helper thread
+ * computes make_params of the next frames while this thread launches the current one, so a
+ * frame costs the host max(arguments, launch) instead of their sum.  Same launches, same
+ * order, same arguments as the sequential loop. */
+static int render_frames_pipelined(rt_ctx* ctx, const rt_camera* cams, int32_t ncams, int32_t row0,
+                                   int32_t nrows, int32_t depth, int32_t precision, uint32_t flags,
+                                   int32_t out_format, void* const* d_outs, int32_t nouts,
+                                   void* const* streams, int32_t nstreams, int32_t nframes) {
+    if (!ctx->prep) {
+        ctx->prep = new (std::nothrow) rt_ctx::Prep();
+        if (!ctx->prep) return RT_ERR_OUT_OF_MEMORY;
+        try {
+            ctx->prep->th = std::thread(prep_main, ctx);
+        } catch (...) {
+            delete ctx->prep;
+            ctx->prep = nullptr;
+            return RT_ERR_OUT_OF_MEMORY;
+        }
+    }
+    rt_ctx::Prep& q = *ctx->prep;
+    q.cams = cams;
+    q.ncams = ncams;
+    q.row0 = row0;
+    q.nrows = nrows;
+    q.depth = depth;
+    q.precision = precision;
+    q.flags = flags;
+    q.out_format = out_format;
+    q.d_outs = d_outs;
+    q.nouts = nouts;
+    q.nframes = nframes;
+    q.produced.store(0, std::memory_order_relaxed);
+    q.consumed.store(0, std::memory_order_relaxed);
+    q.stop.store(false, std::memory_order_relaxed);
+    uint64_t g;
+    {
+        std::lock_guard<std::mutex> lk(q.mu);
+        g = q.posted.load(std::memory_order_relaxed) + 1;
+        q.posted.store(g, std::memory_order_release);
+    }
+    q.cv.notify_one();
+    int st = RT_OK;
+    for (int32_t f = 0; f < nframes; f++) {
+        while (q.produced.load(std::memory_order_acquire) <= f) std::this_thread::yield();
+        void* stf = nstreams > 0 ? streams[f % nstreams] : nullptr;
+        st = render_device_impl(ctx, &cams[f % ncams], row0, nrows, 0, 0, 0, depth, precision, flags,
+                                out_format, d_outs[f % nouts], nullptr, stf,
+                                &q.slot[f % rt_ctx::Prep::RING]);
+        q.consumed.store(f + 1, std::memory_order_release);
+        if (st != RT_OK) break;
+    }
+    // the helper is done with this batch before its arguments (cams, d_outs) go out of scope
+    q.stop.store(true, std::memory_order_release);
+    while (q.done.load(std::memory_order_acquire) != g) std::this_thread::yield();
+    return st;
+}
+
 int rt_render_device_frames(rt_ctx* ctx, const rt_camera* cams, int32_t ncams, int32_t row0,
                             int32_t nrows, int32_t depth, int32_t precision, uint32_t flags,
                             int32_t out_format, void* const* d_outs, int32_t nouts,
@@ -1565,6 +1710,19 @@ int rt_render_device_frames(rt_ctx* ctx, const rt_camera* cams, int32_t ncams, i
     if (!ctx || !cams || ncams <= 0 || !d_outs || nouts <= 0 || nframes < 0 ||
         (nstreams > 0 && !streams) || nstreams < 0)
         return RT_ERR_INVALID_ARG;
+    if (ctx->host_pipeline && nframes >= 2 && !RT_DRY_LAUNCH) {
+        // every frame's arguments checked up front (the pipeline's helper computes them
+        // unchecked); a batch with an invalid frame takes the sequential loop, which stops
+        // at that frame with its status
+        bool ok = true;
+        for (int32_t c = 0; c < ncams && c < nframes && ok; c++)
+            ok = check_render_args(ctx, &cams[c], row0, nrows, depth, precision, out_format) == RT_OK;
+        for (int32_t f = 0; f < nframes && f < nouts && ok; f++)
+            ok = d_outs[f] != nullptr || nrows == 0 || cams[f % ncams].width == 0;
+        if (ok)
+            return render_frames_pipelined(ctx, cams, ncams, row0, nrows, depth, precision, flags,
+                                           out_format, d_outs, nouts, streams, nstreams, nframes);
+    }
     for (int32_t f = 0; f < nframes; f++) {
         void* st = nstreams > 0 ? streams[f % nstreams] : nullptr;
         const int e = rt_render_device(ctx, &cams[f % ncams], row0, nrows, depth, precision,
@@ -1667,3 +1825,46 @@ int rt_tile_row_costs(rt_ctx* ctx, const rt_camera* cam, int32_t depth, int32_t 
     }
     return RT_OK;
 }
+
+#if RT_HOST_BENCH
+/* Diagnostic build only (-DRT_HOST_BENCH=1, tools/host_bench.py): the per-frame host work of
+ * a render, timed on the CPU with no device — out_us[0] = make_params (everything the host
+ * computes per frame), [1] = frame_boxes alone, [2] = the KParams value-init + copy. */
+extern "C" int rt_host_bench(const rt_prim* prims, int32_t n, const rt_camera* cam, int32_t row0,
+                             int32_t nrows, int32_t iters, double* out_us) {
+    std::unique_ptr<rt_ctx> ctx(new rt_ctx());
+    const int st = pack_scene(prims, n, ctx->sc);
+    if (st != RT_OK) return st;
+    ctx->have_scene = true;
+    ctx->wave_cull_min = 0x7fffffff;
+    std::unique_ptr<rt::KParams> p(new rt::KParams);
+    using clk = std::chrono::steady_clock;
+    auto us = [](clk::time_point a, clk::time_point b) {
+        return std::chrono::duration<double, std::micro>(b - a).count();
+    };
+    volatile int sink = 0;
+    auto t0 = clk::now();
+    for (int k = 0; k < iters; k++) {
+        *p = make_params(ctx.get(), cam, row0, nrows, 4, 0, RT_OUT_RGB_F32, nullptr, nullptr, RT_PREC_PATH64);
+        sink += p->nbox;
+    }
+    auto t1 = clk::now();
+    for (int k = 0; k < iters; k++) {
+        frame_boxes(ctx.get(), cam, row0, nrows, *p);
+        sink += p->nbox;
+    }
+    auto t2 = clk::now();
+    for (int k = 0; k < iters; k++) {
+        rt::KParams q{};
+        q.nbox = k;
+        *p = q;
+        sink += p->nbox;
+    }
+    auto t3 = clk::now();
+    out_us[0] = us(t0, t1) / iters;
+    out_us[1] = us(t1, t2) / iters;
+    out_us[2] = us(t2, t3) / iters;
+    (void)sink;
+    return RT_OK;
+}
+#endif

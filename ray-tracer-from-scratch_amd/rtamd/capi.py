@@ -66,6 +66,7 @@ RT_OPT_ROW_FEEDBACK_WARM = 10
 RT_OPT_WALL_ORDER = 11
 RT_OPT_CLUSTER_COS = 12
 RT_OPT_MULTI_LAYOUT = 13
+RT_OPT_HOST_PIPELINE = 16
 RT_OPT_ROW_FEEDBACK_EMA = 14
 RT_OPT_ROW_FEEDBACK_ISOLATE = 15
 

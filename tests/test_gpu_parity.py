@@ -451,6 +451,30 @@ def test_non_integer_specular_exponent(rend, oracle):
                 check_f32(img, o64, sig, 5, ("nonint f32", w))
 
 
+def test_path64_full_size_c5_vs_oracle_sampled_rows(rend, oracle):
+    """The bench precision at BASELINE config 5's full size against the pinned oracle, not
+    only against F64: one full 7680x4320 PATH64 frame (depth 8, 256 spheres, the cull +
+    sphere-cluster kernels at their defaults), and 32 blocks of 8 rows spread evenly over
+    the frame (256 rows, through the sphere cloud) traced by the oracle — every pixel of
+    them within PATH64_TOL, and each block's segment count equal to the oracle's."""
+    cfg = scenes.CONFIGS["c5"]
+    prims = scenes.to_prims(cfg.scene())
+    rend.set_scene(prims)
+    cam = capi.camera_init(**scenes.camera_args(cfg.width, cfg.height))
+    full, _ = rend.render(cam, cfg.depth, capi.RT_PREC_PATH64, 0, capi.RT_OUT_RGB_F32)
+    starts = [int(round(k * (cfg.height - 8) / 31)) for k in range(32)]
+    worst = 0.0
+    for r0 in starts:
+        o64, _, segs = oracle.render(prims, cam, cfg.depth, row0=r0, nrows=8, nthreads=NTHREADS)
+        _, st = rend.render(cam, cfg.depth, capi.RT_PREC_PATH64, 0, capi.RT_OUT_RGB_F32,
+                            row0=r0, nrows=8, count_segments=True)
+        assert st.segments == segs, (r0, st.segments, segs)
+        d = float(np.abs(full[r0:r0 + 8] - o64).max())
+        worst = max(worst, d)
+        assert d <= PATH64_TOL, (r0, d)
+    assert worst > 0.0   # fp32 colour: not bit-equal to the fp64 oracle, only within the bar
+
+
 def test_path64_full_size_c5_vs_f64(rend):
     """BASELINE config 5 (7680x4320, 256 spheres, depth 8) at full size in the bench
     precision with the sphere-cluster path at its default: PATH64's ray paths are F64's
@@ -807,16 +831,31 @@ def test_render_device_frames_equals_per_frame_calls(rend):
     a["position"] = (ca["position"][0] + 0.3, ca["position"][1], ca["position"][2])
     cams.append(capi.camera_init(**a))
     refs = [rend.render(c, 4, capi.RT_PREC_PATH64, 0, capi.RT_OUT_RGB_F32)[0] for c in cams]
-    outs = [torch.zeros((90, 160, 3), dtype=torch.float32, device=dev) for _ in range(3)]
     sts = [torch.cuda.Stream(dev) for _ in range(3)]
-    rend.render_device_frames(cams, 4, [o.data_ptr() for o in outs], capi.RT_PREC_PATH64,
-                              streams=[s.cuda_stream for s in sts], nframes=7)
-    torch.cuda.synchronize()
-    last_cam = {0: 0, 1: 0, 2: 1}  # frames 6, 4, 5
-    for b, o in enumerate(outs):
-        assert np.array_equal(o.cpu().numpy().view(np.uint32), refs[last_cam[b]].view(np.uint32))
-    with pytest.raises(capi.RTError):
-        rend.render_device_frames(cams, 4, [], capi.RT_PREC_PATH64, nframes=1)
+    # with the host pipeline (the default: the next frames' arguments on a helper thread) and
+    # without it; batches of 1 (no helper), 7 and 40 frames
+    for pipe in (1, 0):
+        rend.set_option(capi.RT_OPT_HOST_PIPELINE, pipe)
+        for nf in (1, 7, 40):
+            outs = [torch.zeros((90, 160, 3), dtype=torch.float32, device=dev) for _ in range(3)]
+            torch.cuda.synchronize()
+            rend.render_device_frames(cams, 4, [o.data_ptr() for o in outs], capi.RT_PREC_PATH64,
+                                      streams=[s.cuda_stream for s in sts], nframes=nf)
+            torch.cuda.synchronize()
+            for b, o in enumerate(outs):
+                fr = [f for f in range(nf) if f % 3 == b]
+                want = refs[fr[-1] % 2] if fr else np.zeros_like(refs[0])
+                assert np.array_equal(o.cpu().numpy().view(np.uint32), want.view(np.uint32)), (pipe, nf, b)
+        with pytest.raises(capi.RTError):
+            rend.render_device_frames(cams, 4, [], capi.RT_PREC_PATH64, nframes=1)
+        # a batch whose second camera is invalid stops there with its status, pipeline or not
+        bad = capi.camera_init(**ca)
+        bad.height = -1
+        with pytest.raises(capi.RTError):
+            rend.render_device_frames([cams[0], bad], 4, [o.data_ptr() for o in outs],
+                                      capi.RT_PREC_PATH64, streams=[sts[0].cuda_stream], nframes=4)
+        torch.cuda.synchronize()
+    rend.set_option(capi.RT_OPT_HOST_PIPELINE, 1)
 
 
 def test_row_feedback_isolated_sampling_in_flight(rend):
