@@ -40,6 +40,12 @@ import sys
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
+# N > 1: every rank keeps RT_OPT_MULTI_FRAMES (4) band frames in flight on their own streams,
+# which need their own hardware queues (HIP's default is 4 per process, shared round-robin by
+# every stream the process makes: with it 4 band frames in flight were no faster than 2 —
+# tools/band_model.py).  Read by the HIP runtime at its initialisation.
+if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
 sys.path.insert(0, os.path.join(REPO, "ray-tracer-from-scratch_amd"))
 
 from rtamd import capi, scenes  # noqa: E402
@@ -159,6 +165,8 @@ def main() -> int:
                          "(rt_band_rows), or contiguous bands cut so each carries 1/N of the "
                          "tile-row costs rank 0 measures once on its GPU and broadcasts "
                          "(rt_weighted_band_rows, RT_OPT_MULTI_LAYOUT 2)")
+    ap.add_argument("--rank-frames", type=int, default=4,
+                    help="N > 1: band frames in flight per rank (RT_OPT_MULTI_FRAMES)")
     ap.add_argument("--local-ranks", type=int, default=1,
                     help="rehearsal only (one process): split the frame over this many ranks "
                          "on this one GPU with the peer-copy transport; not a measurement")
@@ -300,6 +308,8 @@ def main() -> int:
         if layout == 2:
             multi.set_row_weights(weights)
         multi.set_option(capi.RT_OPT_MULTI_LAYOUT, layout)
+        if multi.nranks > 1:
+            multi.set_option(capi.RT_OPT_MULTI_FRAMES, max(1, min(capi.RT_MULTI_SLOTS, args.rank_frames)))
     elif tiled_mode:
         from rtamd import tiling
         # double-buffered: the gather of frame k (collective stream) overlaps the render of k+1
@@ -763,6 +773,8 @@ def main() -> int:
                 "parallelism": par,
                 "band_rows_rank0": nrows,
                 "band_layout": args.band_layout if (tiled_mode and (world > 1 or args.local_ranks > 1)) else None,
+                "rank_frames_in_flight": args.rank_frames if (tiled_mode and (world > 1 or args.local_ranks > 1)) else None,
+                "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
                 "host_box_cache": bool(args.box_cache),
                 "row_feedback": args.row_feedback,
                 "frames_in_flight": fif,

@@ -214,6 +214,13 @@ enum rt_option {
                                          calling thread launches the current frame; 0 = one
                                          thread does both in turn.  The same launches in the
                                          same order: output is identical. */
+    RT_OPT_MULTI_FRAMES = 17,        /* rt_multi_set_option only: F in [1, RT_MULTI_SLOTS]
+                                         (default 2) band slots per rank — frames of a rank in
+                                         flight on F render streams, so a small band's longest
+                                         waves (a 1/8 band of config 4: tiles bouncing between
+                                         facing walls) overlap F - 1 other frames.  Every
+                                         handle of one exchange must use the same F.  The
+                                         gathered frames are identical. */
     RT_OPT_MULTI_LAYOUT = 13,        /* rt_multi_set_option only: 0 (default) = contiguous
                                          row bands (rt_band_rows); 1 = interleaved tile rows
                                          (rt_interleaved_rows): balanced when the frame's cost
@@ -293,8 +300,9 @@ int rt_render_device_frames(rt_ctx* ctx, const rt_camera* cams, int32_t ncams, i
  * group as the other bands' receives) and a communicator even at one rank — so every RCCL
  * call of the gather (ncclCommInitRank, the group, send/recv, ncclCommGetAsyncError)
  * executes on a one-GPU machine; it costs one extra copy of the root's band.
- * Frames in flight: each non-root rank renders into one of RT_MULTI_SLOTS band buffers on
- * its render stream while the previous frame's band is still being sent on its comm stream;
+ * Frames in flight: each non-root rank renders into one of RT_OPT_MULTI_FRAMES (<=
+ * RT_MULTI_SLOTS) band buffers, each with its own render stream, while earlier frames' bands
+ * are still being rendered or sent on its comm stream;
  * a band buffer is reused only after its send has completed (device-side event waits; the
  * host never blocks in rt_multi_render_device*).
  * Failures: a frame that fails on one rank after a local rank has queued its part of the
@@ -307,7 +315,7 @@ int rt_render_device_frames(rt_ctx* ctx, const rt_camera* cams, int32_t ncams, i
  * failure: the other processes are not told, and their sends, receives or rt_multi_sync can
  * block until their own communicator is aborted (RT_TRANSPORT_THREADS does tell its peers). */
 #define RT_MULTI_ID_BYTES 128
-#define RT_MULTI_SLOTS 2
+#define RT_MULTI_SLOTS 4   /* band slots per rank (RT_OPT_MULTI_FRAMES uses 1..4, default 2) */
 enum rt_transport {
     RT_TRANSPORT_RCCL = 0,
     RT_TRANSPORT_COPY = 1,

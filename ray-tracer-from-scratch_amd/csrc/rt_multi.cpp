@@ -16,7 +16,7 @@
  *     buffer may still be read), receives every other band into its rows (one
  *     ncclGroupStart/End), and the caller's stream waits for it.
  *   other ranks: slot s's render stream waits until band buffer s has been sent (frame
- *     k - RT_MULTI_SLOTS), renders the band into it, and the comm stream sends it once the
+ *     k - slots, RT_OPT_MULTI_FRAMES), renders the band into it, and the comm stream sends it once the
  *     render is done (RCCL ncclSend, or a peer copy into the root's rows for
  *     RT_TRANSPORT_COPY) — so the render of frame k+1 overlaps the send of frame k, and the
  *     tail of frame k's band kernel (one slot's stream) overlaps frame k+1's (the other's).
@@ -76,17 +76,17 @@ struct Rank {
     // one render stream per band slot: consecutive frames' band kernels overlap, so a rank's
     // frame rate is not bounded by its heaviest wave's latency (a c2 band's kernel takes
     // ~20 us for 1/8 of the frame: the tail, tools/band_model.py)
-    hipStream_t render_stream[RT_MULTI_SLOTS] = {nullptr, nullptr};
+    hipStream_t render_stream[RT_MULTI_SLOTS] = {};
     hipStream_t comm_stream = nullptr;
-    void* band[RT_MULTI_SLOTS] = {nullptr, nullptr};
+    void* band[RT_MULTI_SLOTS] = {};
     size_t band_cap = 0;
-    hipEvent_t ev_rendered[RT_MULTI_SLOTS] = {nullptr, nullptr};
-    hipEvent_t ev_sent[RT_MULTI_SLOTS] = {nullptr, nullptr};
+    hipEvent_t ev_rendered[RT_MULTI_SLOTS] = {};
+    hipEvent_t ev_sent[RT_MULTI_SLOTS] = {};
     hipEvent_t ev_done = nullptr;   // root, RCCL / THREADS: every band received
-    hipEvent_t ev_ready[RT_MULTI_SLOTS] = {nullptr, nullptr};  // root, THREADS: parts may land
+    hipEvent_t ev_ready[RT_MULTI_SLOTS] = {};  // root, THREADS: parts may land
     // root, RCCL, interleaved layout: every rank's part received here, then scattered into
     // its frame rows (one strided copy per part)
-    void* staging[RT_MULTI_SLOTS] = {nullptr, nullptr};
+    void* staging[RT_MULTI_SLOTS] = {};
     size_t staging_cap = 0;
     // worker thread (local ranks other than the first, one process driving several GPUs)
     std::thread th;
@@ -122,12 +122,13 @@ std::map<std::string, std::shared_ptr<Hub>> g_hubs;
 
 struct rt_multi {
     int nranks = 1, nlocal = 1, first_rank = 0, transport = RT_TRANSPORT_RCCL;
+    int slots = 2;                  // RT_OPT_MULTI_FRAMES: band slots in use (frames in flight)
     int layout = 0;                 // RT_OPT_MULTI_LAYOUT: 0 contiguous bands, 1 interleaved,
                                     // 2 contiguous bands weighted by `weights`
     std::vector<float> weights;     // rt_multi_set_row_weights: per tile row
     std::vector<Rank*> r;           // local ranks, r[0] = first_rank
     uint64_t frame = 0;
-    hipEvent_t ev_in[RT_MULTI_SLOTS] = {nullptr, nullptr};  // root's device (process with root)
+    hipEvent_t ev_in[RT_MULTI_SLOTS] = {};  // root's device (process with root)
     hipStream_t host_stream = nullptr;                       // rt_multi_render (root's device)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     void* d_frame = nullptr;
@@ -466,7 +467,7 @@ int enqueue_rank(rt_multi* m, Rank* k, const Job& j) {
     if (bytes == 0) return RT_OK;  // an empty band (height < nranks): nothing to render or send
     st = ensure_bands(m, k, (size_t)max_part_rows(m, cam.height) * row_bytes);
     if (st != RT_OK) return st;
-    // band buffer `s` is free once the send of frame k - RT_MULTI_SLOTS has completed
+    // band buffer `s` is free once the send of frame k - slots has completed
     MHIPF(m, hipStreamWaitEvent(k->render_stream[s], k->ev_sent[s], 0));
     {
         SlowCall sc_("rt_render_device (band)");
@@ -585,7 +586,7 @@ int render_frame(rt_multi* m, const rt_camera* cam, int32_t depth, int32_t preci
                       "an earlier frame failed after the gather was queued: the communicator is out of step");
         return RT_ERR_COMM;
     }
-    const int slot = (int)(m->frame % RT_MULTI_SLOTS);
+    const int slot = (int)(m->frame % (uint64_t)m->slots);
     m->queued.store(false, std::memory_order_relaxed);
     Job j;
     j.cam = cam;
@@ -863,6 +864,13 @@ int rt_multi_set_scene(rt_multi* m, const rt_prim* prims, int32_t n) {
 
 int rt_multi_set_option(rt_multi* m, int32_t option, int64_t value) {
     if (!m) return RT_ERR_INVALID_ARG;
+    if (option == RT_OPT_MULTI_FRAMES) {
+        if (value < 1 || value > RT_MULTI_SLOTS) return RT_ERR_INVALID_ARG;
+        const int st = rt_multi_sync(m);  // frames in flight keep the slots they started with
+        if (st != RT_OK) return st;
+        m->slots = (int)value;
+        return RT_OK;
+    }
     if (option == RT_OPT_MULTI_LAYOUT) {
         if (value < 0 || value > 2) return RT_ERR_INVALID_ARG;
         const int st = rt_multi_sync(m);  // frames in flight keep the layout they started with

@@ -34,7 +34,7 @@ RT_TRANSPORT_COPY = 1
 RT_TRANSPORT_RCCL_LOOPBACK = 2
 RT_TRANSPORT_THREADS = 3   # rehearsal: one handle per rank in one process (include/rt_capi.h)
 RT_MULTI_ID_BYTES = 128
-RT_MULTI_SLOTS = 2
+RT_MULTI_SLOTS = 4
 
 RT_PRIM_SPHERE = 0
 RT_PRIM_WALL = 1
@@ -67,6 +67,7 @@ RT_OPT_WALL_ORDER = 11
 RT_OPT_CLUSTER_COS = 12
 RT_OPT_MULTI_LAYOUT = 13
 RT_OPT_HOST_PIPELINE = 16
+RT_OPT_MULTI_FRAMES = 17
 RT_OPT_ROW_FEEDBACK_EMA = 14
 RT_OPT_ROW_FEEDBACK_ISOLATE = 15
 

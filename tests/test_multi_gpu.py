@@ -91,9 +91,11 @@ def test_ragged_and_empty_bands(rend, n, w, h):
         assert np.array_equal(got.view(np.uint64), ref.view(np.uint64))
 
 
-@pytest.mark.parametrize("transport,n", [(capi.RT_TRANSPORT_COPY, 4), (capi.RT_TRANSPORT_RCCL, 1),
-                                         (capi.RT_TRANSPORT_RCCL_LOOPBACK, 1)])
-def test_frames_in_flight_on_caller_streams(rend, transport, n):
+@pytest.mark.parametrize("transport,n,frames", [(capi.RT_TRANSPORT_COPY, 4, 2), (capi.RT_TRANSPORT_COPY, 4, 4),
+                                                (capi.RT_TRANSPORT_RCCL, 1, 2),
+                                                (capi.RT_TRANSPORT_RCCL_LOOPBACK, 1, 2),
+                                                (capi.RT_TRANSPORT_RCCL_LOOPBACK, 1, 3)])
+def test_frames_in_flight_on_caller_streams(rend, transport, n, frames):
     """The bench's frame loop: many frames of a moving camera enqueued back to back by one
     rt_multi_render_device_frames call into two device frame buffers on two caller streams
     (band slots reused every RT_MULTI_SLOTS frames while earlier sends may be in flight).
@@ -112,6 +114,7 @@ def test_frames_in_flight_on_caller_streams(rend, transport, n):
     torch.cuda.synchronize()
     with capi.MultiRenderer([0] * n, transport=transport) as m:
         m.set_scene(prims)
+        m.set_option(capi.RT_OPT_MULTI_FRAMES, frames)
         nf = 13
         m.render_device_frames(cams, 4, [b.data_ptr() for b in bufs], capi.RT_PREC_PATH64,
                                streams=[s.cuda_stream for s in sts], nframes=nf)
@@ -255,6 +258,9 @@ def test_multi_interleaved_layout_bitwise(rend, n):
                 assert np.array_equal(b.cpu().numpy().view(np.uint32), ref.view(np.uint32)), (n, w)
         with pytest.raises(capi.RTError):
             m.set_option(capi.RT_OPT_MULTI_LAYOUT, 3)
+        for bad in (0, capi.RT_MULTI_SLOTS + 1):
+            with pytest.raises(capi.RTError):
+                m.set_option(capi.RT_OPT_MULTI_FRAMES, bad)
 
 
 def test_loopback_rccl_c4_full_size_frames_in_flight(rend):
@@ -336,8 +342,8 @@ def _run_threads(handles, fn):
     return errs
 
 
-@pytest.mark.parametrize("n,layout", [(2, 0), (3, 1), (8, 1), (4, 2), (8, 2)])
-def test_threads_transport_runs_the_process_per_gpu_branches(rend, n, layout):
+@pytest.mark.parametrize("n,layout,frames", [(2, 0, 2), (3, 1, 2), (8, 1, 4), (4, 2, 3), (8, 2, 4)])
+def test_threads_transport_runs_the_process_per_gpu_branches(rend, n, layout, frames):
     """RT_TRANSPORT_THREADS: n rt_multi handles in this process, one per rank (nlocal = 1,
     first_rank = r, one shared id), each driven from its own thread exactly as the
     process-per-GPU bench drives its rank — so the branches the first multi-GPU run takes
@@ -348,9 +354,10 @@ def test_threads_transport_runs_the_process_per_gpu_branches(rend, n, layout):
     into its staging buffers then scattered by strided copies (layout 1: the staging
     allocation, slot reuse and scatter of the RCCL path), cost-weighted bands (layout 2).
     Config 4's full frame (1920x1080, c2 scene, depth 4), 7 frames of a moving camera in
-    flight over two root buffers: every buffer is bitwise the one-GPU frame of the last camera
-    written to it, and a rank's band is already in the root's frame when its caller stream
-    has passed the frame (checked on the last frame)."""
+    flight over two root buffers, 2-4 band slots per rank (RT_OPT_MULTI_FRAMES): every buffer
+    is bitwise the one-GPU frame of the last camera written to it, and a rank's band is
+    already in the root's frame when its caller stream has passed the frame (checked on the
+    last frame)."""
     import os
     import torch
     dev = torch.device("cuda", 0)
@@ -374,6 +381,7 @@ def test_threads_transport_runs_the_process_per_gpu_branches(rend, n, layout):
         for h in hs:
             h.set_scene(prims)
             h.set_option(capi.RT_OPT_MULTI_LAYOUT, layout)
+            h.set_option(capi.RT_OPT_MULTI_FRAMES, frames)
             if weights is not None:
                 h.set_row_weights(weights)
         torch.cuda.synchronize()
