@@ -221,6 +221,10 @@ enum rt_option {
                                          facing walls) overlap F - 1 other frames.  Every
                                          handle of one exchange must use the same F.  The
                                          gathered frames are identical. */
+    RT_OPT_MULTI_FAULT = 18,         /* rt_multi_set_option only, a test hook: 1 = the next
+                                         frame of the process holding the root fails right
+                                         after its RCCL receives were queued (the failure
+                                         path of a real exchange on a one-GPU machine). */
     RT_OPT_MULTI_LAYOUT = 13,        /* rt_multi_set_option only: 0 (default) = contiguous
                                          row bands (rt_band_rows); 1 = interleaved tile rows
                                          (rt_interleaved_rows): balanced when the frame's cost

@@ -123,6 +123,7 @@ std::map<std::string, std::shared_ptr<Hub>> g_hubs;
 struct rt_multi {
     int nranks = 1, nlocal = 1, first_rank = 0, transport = RT_TRANSPORT_RCCL;
     int slots = 2;                  // RT_OPT_MULTI_FRAMES: band slots in use (frames in flight)
+    bool fault_next = false;        // RT_OPT_MULTI_FAULT (test hook)
     int layout = 0;                 // RT_OPT_MULTI_LAYOUT: 0 contiguous bands, 1 interleaved,
                                     // 2 contiguous bands weighted by `weights`
     std::vector<float> weights;     // rt_multi_set_row_weights: per tile row
@@ -452,6 +453,11 @@ int enqueue_rank(rt_multi* m, Rank* k, const Job& j) {
                 }
             }
             MNCCL(m, ncclGroupEnd());
+            if (m->fault_next) {  // RT_OPT_MULTI_FAULT (tests): fail once the gather is queued
+                m->fault_next = false;
+                std::snprintf(m->last_err, sizeof m->last_err, "injected fault after the gather was queued");
+                return RT_ERR_HIP;
+            }
             if (inter)
                 for (int g = lb ? 0 : 1; g < m->nranks; g++) {
                     st = scatter_part(m, j.d_frame, static_cast<char*>(k->staging[s]) + (size_t)g * part_bytes,
@@ -864,6 +870,11 @@ int rt_multi_set_scene(rt_multi* m, const rt_prim* prims, int32_t n) {
 
 int rt_multi_set_option(rt_multi* m, int32_t option, int64_t value) {
     if (!m) return RT_ERR_INVALID_ARG;
+    if (option == RT_OPT_MULTI_FAULT) {
+        if (value != 0 && value != 1) return RT_ERR_INVALID_ARG;
+        m->fault_next = value == 1;
+        return RT_OK;
+    }
     if (option == RT_OPT_MULTI_FRAMES) {
         if (value < 1 || value > RT_MULTI_SLOTS) return RT_ERR_INVALID_ARG;
         const int st = rt_multi_sync(m);  // frames in flight keep the slots they started with

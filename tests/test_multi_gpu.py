@@ -321,6 +321,33 @@ def test_failure_before_the_gather_is_queued_keeps_the_communicator(rend):
         m.close()
 
 
+def test_failure_after_the_gather_is_queued_breaks_the_communicator(rend):
+    """A frame that fails after the root's RCCL receives were queued (RT_OPT_MULTI_FAULT
+    injects exactly that on the loopback communicator) leaves the exchange out of step: the
+    rt_multi reports RT_ERR_COMM on every later frame and on rt_multi_sync (which aborts the
+    communicator, ncclCommAbort, instead of waiting), and destroying it returns."""
+    import torch
+    dev = torch.device("cuda", 0)
+    cam = _cam(64, 36)
+    buf = torch.zeros((36, 64, 3), device=dev)
+    m = capi.MultiRenderer([0], transport=capi.RT_TRANSPORT_RCCL_LOOPBACK)
+    try:
+        m.set_scene(scenes.to_prims(scenes.synthetic_scene(8, 4)))
+        m.render_device(cam, 2, buf.data_ptr(), capi.RT_PREC_PATH64)   # a healthy frame first
+        m.set_option(capi.RT_OPT_MULTI_FAULT, 1)
+        with pytest.raises(capi.RTError) as e1:
+            m.render_device(cam, 2, buf.data_ptr(), capi.RT_PREC_PATH64)
+        assert e1.value.status == capi.RT_ERR_HIP
+        with pytest.raises(capi.RTError) as e2:
+            m.render_device(cam, 2, buf.data_ptr(), capi.RT_PREC_PATH64)
+        assert e2.value.status == capi.RT_ERR_COMM
+        with pytest.raises(capi.RTError) as e3:
+            m.sync()
+        assert e3.value.status == capi.RT_ERR_COMM
+    finally:
+        m.close()
+
+
 def _run_threads(handles, fn):
     """Drive every THREADS handle from its own thread (as one process per GPU would) and
     return the per-rank exceptions (None = ok)."""
