@@ -956,6 +956,26 @@ int rt_multi_render_device_frames(rt_multi* m, const rt_camera* cams, int32_t nc
         (nbufs > 0 && !d_frames) || (nstreams > 0 && !streams))
         return RT_ERR_INVALID_ARG;
     if (m->has_root() && nbufs == 0) return RT_ERR_INVALID_ARG;
+    if (m->nranks == 1 && !m->gathers() && !m->broken && nstreams > 0 && nframes > 1) {
+        // one rank and no exchange: the band is the frame, rendered in place on the caller's
+        // streams, so the batch is the ctx's own frame loop (rt_render_device_frames, with
+        // its host pipeline) — the same launches as frame-by-frame render_frame
+        bool same = true;
+        for (int32_t s = 0; s < nstreams; s++) same = same && streams[s] != nullptr;
+        for (int32_t c = 0; c < ncams && c < nframes; c++)
+            same = same && cams[c].height == cams[0].height &&
+                   check_args(m, &cams[c], depth, precision, out_format) == RT_OK;
+        if (same) {
+            Rank* k = m->r[0];
+            const int st = ctx_err(m, k,
+                                   rt_render_device_frames(k->ctx, cams, ncams, 0, cams[0].height, depth,
+                                                           precision, flags, out_format, d_frames, nbufs,
+                                                           streams, nstreams, nframes),
+                                   "rt_render_device_frames");
+            m->frame += (uint64_t)nframes;
+            return st;
+        }
+    }
     for (int32_t f = 0; f < nframes; f++) {
         const rt_camera* cam = &cams[f % ncams];
         int st = check_args(m, cam, depth, precision, out_format);

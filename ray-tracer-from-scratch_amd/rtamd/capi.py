@@ -69,7 +69,6 @@ RT_OPT_MULTI_LAYOUT = 13
 RT_OPT_HOST_PIPELINE = 16
 RT_OPT_MULTI_FRAMES = 17
 RT_OPT_MULTI_FAULT = 18
-RT_OPT_STAGGER_NS = 19
 RT_OPT_ROW_FEEDBACK_EMA = 14
 RT_OPT_ROW_FEEDBACK_ISOLATE = 15
 
