@@ -167,6 +167,10 @@ def main() -> int:
                          "(rt_weighted_band_rows, RT_OPT_MULTI_LAYOUT 2)")
     ap.add_argument("--rank-frames", type=int, default=4,
                     help="N > 1: band frames in flight per rank (RT_OPT_MULTI_FRAMES)")
+    ap.add_argument("--rank-batch", type=int, default=4,
+                    help="N > 1: frames per gather (RT_OPT_MULTI_BATCH): each rank sends its bands "
+                         "of that many frames in one ncclSend, the root scatters them with one "
+                         "kernel (the per-frame exchange's host calls cost more than a 1/8 band)")
     ap.add_argument("--local-ranks", type=int, default=1,
                     help="rehearsal only (one process): split the frame over this many ranks "
                          "on this one GPU with the peer-copy transport; not a measurement")
@@ -310,6 +314,7 @@ def main() -> int:
         multi.set_option(capi.RT_OPT_MULTI_LAYOUT, layout)
         if multi.nranks > 1:
             multi.set_option(capi.RT_OPT_MULTI_FRAMES, max(1, min(capi.RT_MULTI_SLOTS, args.rank_frames)))
+            multi.set_option(capi.RT_OPT_MULTI_BATCH, max(1, min(capi.RT_MULTI_BATCH_MAX, args.rank_batch)))
     elif tiled_mode:
         from rtamd import tiling
         # double-buffered: the gather of frame k (collective stream) overlaps the render of k+1
@@ -341,14 +346,18 @@ def main() -> int:
             # ncclSend/ncclRecv, ncclCommGetAsyncError all run)
             chk = capi.MultiRenderer([local], transport=capi.RT_TRANSPORT_RCCL_LOOPBACK)
             chk.set_option(capi.RT_OPT_ROW_FEEDBACK, args.row_feedback)
+            # the batched exchange the N > 1 runs use (its three frames in one batch)
+            chk.set_option(capi.RT_OPT_MULTI_BATCH, max(1, min(capi.RT_MULTI_BATCH_MAX, args.rank_batch)))
             chk.set_scene(prims)
             op_name = ("rt_multi, RT_TRANSPORT_RCCL_LOOPBACK: RCCL send/recv of the one band "
-                       "through a one-rank communicator (the timed N = 1 loop renders in place)")
+                       "through a one-rank communicator, batched as the N > 1 runs are "
+                       f"(RT_OPT_MULTI_BATCH {args.rank_batch}; the timed N = 1 loop renders in place)")
         elif multi is not None:
             op_name = (f"rt_multi, {multi.nranks} ranks, "
                        + ("RCCL send/recv" if args.transport == "rccl" and world > 1
                           else "peer copies (rehearsal)")
-                       + f", {args.band_layout} bands")
+                       + f", {args.band_layout} bands"
+                       + (f", {args.rank_batch} frames per gather" if world > 1 else ""))
         if chk is not None:
             outs[0].fill_(-1.0)
             torch.cuda.synchronize(dev)
@@ -774,6 +783,7 @@ def main() -> int:
                 "band_rows_rank0": nrows,
                 "band_layout": args.band_layout if (tiled_mode and (world > 1 or args.local_ranks > 1)) else None,
                 "rank_frames_in_flight": args.rank_frames if (tiled_mode and (world > 1 or args.local_ranks > 1)) else None,
+                "frames_per_gather": args.rank_batch if (tiled_mode and world > 1) else None,
                 "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
                 "host_box_cache": bool(args.box_cache),
                 "row_feedback": args.row_feedback,

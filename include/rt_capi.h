@@ -225,6 +225,19 @@ enum rt_option {
                                          frame of the process holding the root fails right
                                          after its RCCL receives were queued (the failure
                                          path of a real exchange on a one-GPU machine). */
+    RT_OPT_MULTI_BATCH = 19,         /* rt_multi_set_option only: B in [1,
+                                         RT_MULTI_BATCH_MAX] (default 1) frames per gather in
+                                         rt_multi_render_device_frames, one process per rank
+                                         (nlocal == 1) with contiguous or weighted bands: each
+                                         rank renders B frames' bands back to back and sends
+                                         them in ONE ncclSend; the root receives every rank's
+                                         B bands in one group and scatters them into the B
+                                         frames with one kernel.  The per-frame host work of
+                                         the exchange (events, RCCL calls: ~20 us per frame,
+                                         more than a 1/8 band's kernel) is paid once per B
+                                         frames; a frame's rows reach the root when its batch
+                                         completes.  Every handle of one exchange must use the
+                                         same B and batch sizes.  The frames are identical. */
     RT_OPT_MULTI_LAYOUT = 13,        /* rt_multi_set_option only: 0 (default) = contiguous
                                          row bands (rt_band_rows); 1 = interleaved tile rows
                                          (rt_interleaved_rows): balanced when the frame's cost
@@ -320,6 +333,7 @@ int rt_render_device_frames(rt_ctx* ctx, const rt_camera* cams, int32_t ncams, i
  * block until their own communicator is aborted (RT_TRANSPORT_THREADS does tell its peers). */
 #define RT_MULTI_ID_BYTES 128
 #define RT_MULTI_SLOTS 4   /* band slots per rank (RT_OPT_MULTI_FRAMES uses 1..4, default 2) */
+#define RT_MULTI_BATCH_MAX 16  /* frames per gather (RT_OPT_MULTI_BATCH) */
 enum rt_transport {
     RT_TRANSPORT_RCCL = 0,
     RT_TRANSPORT_COPY = 1,

@@ -88,6 +88,14 @@ struct Rank {
     // its frame rows (one strided copy per part)
     void* staging[RT_MULTI_SLOTS] = {};
     size_t staging_cap = 0;
+    // batched gather (RT_OPT_MULTI_BATCH), two batch slots: a sender's bands of the batch's
+    // frames back to back (bbuf), the root's received parts (bstage); ev_brend: the batch's
+    // bands rendered, ev_bsent: its send complete (bbuf free again)
+    void* bbuf[2] = {};
+    size_t bbuf_cap = 0;
+    void* bstage[2] = {};
+    size_t bstage_cap = 0;
+    hipEvent_t ev_brend[2] = {}, ev_bsent[2] = {};
     // worker thread (local ranks other than the first, one process driving several GPUs)
     std::thread th;
     std::mutex mu;
@@ -123,6 +131,8 @@ std::map<std::string, std::shared_ptr<Hub>> g_hubs;
 struct rt_multi {
     int nranks = 1, nlocal = 1, first_rank = 0, transport = RT_TRANSPORT_RCCL;
     int slots = 2;                  // RT_OPT_MULTI_FRAMES: band slots in use (frames in flight)
+    int batch = 1;                  // RT_OPT_MULTI_BATCH: frames per gather
+    uint64_t nbatch = 0;            // batches gathered (batch slot = nbatch % 2)
     bool fault_next = false;        // RT_OPT_MULTI_FAULT (test hook)
     int layout = 0;                 // RT_OPT_MULTI_LAYOUT: 0 contiguous bands, 1 interleaved,
                                     // 2 contiguous bands weighted by `weights`
@@ -521,6 +531,248 @@ int enqueue_rank(rt_multi* m, Rank* k, const Job& j) {
     return RT_OK;
 }
 
+/* ---- batched gather (RT_OPT_MULTI_BATCH) ----
+ * A batch of kb frames is one exchange: every sender renders its band of the kb frames back
+ * to back into bbuf (the ctx's own frame loop, with its host pipeline, on one render stream)
+ * and sends the kb bands in ONE ncclSend; the root renders its rows of the kb frames in place
+ * on the caller's streams, receives every rank's kb bands into bstage in ONE group, and
+ * copies them into the frames' rows with one scatter kernel.  Two batch slots: batch b + 1
+ * renders while batch b is in flight.  Per frame that is one launch plus 1/kb of the
+ * exchange's calls (events, RCCL), which cost more than a 1/8 band's kernel when paid per
+ * frame (tools/nonroot_host_cost.py). */
+struct ScatterSeg {
+    const char* src;
+    char* dst;
+    uint64_t bytes;
+};
+constexpr int SCATTER_MAX = 128;  // segments per launch (kernel arguments ~3 KB)
+struct ScatterArgs {
+    int32_t nseg, vec16;
+    ScatterSeg seg[SCATTER_MAX];
+};
+/* Segment blockIdx.y: bytes from src to dst, 16 B per lane when every segment allows it. */
+__global__ void __launch_bounds__(256) k_scatter_parts(ScatterArgs a) {
+    const ScatterSeg sg = a.seg[blockIdx.y];
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    const size_t i0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (a.vec16) {
+        const uint4* src = reinterpret_cast<const uint4*>(sg.src);
+        uint4* dst = reinterpret_cast<uint4*>(sg.dst);
+        for (size_t i = i0; i < sg.bytes / 16; i += stride) dst[i] = src[i];
+    } else {
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(sg.src);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(sg.dst);
+        for (size_t i = i0; i < sg.bytes / 4; i += stride) dst[i] = src[i];
+    }
+}
+/* The segments in order (those of frame fidx[j] land in frames[fidx[j]]), one launch per
+ * run in which no frame buffer repeats — a batch that cycles over fewer buffers than frames
+ * lands its frames in frame order, as frame-by-frame gathers would — and at most
+ * SCATTER_MAX segments. */
+int scatter_segments(rt_multi* m, const std::vector<ScatterSeg>& segs, const std::vector<int>& fidx,
+                     char* const* frames, hipStream_t st) {
+    size_t i = 0;
+    while (i < segs.size()) {
+        ScatterArgs a{};
+        std::vector<char*> used;
+        size_t maxb = 0;
+        bool vec = true;
+        size_t j = i;
+        for (; j < segs.size() && a.nseg < SCATTER_MAX; j++) {
+            if (j == i || fidx[j] != fidx[j - 1]) {  // the first segment of a frame
+                char* fb = frames[fidx[j]];
+                if (std::find(used.begin(), used.end(), fb) != used.end()) break;
+                used.push_back(fb);
+            }
+            a.seg[a.nseg++] = segs[j];
+            maxb = std::max<size_t>(maxb, segs[j].bytes);
+            vec = vec && ((reinterpret_cast<uintptr_t>(segs[j].src) | reinterpret_cast<uintptr_t>(segs[j].dst) |
+                           (uintptr_t)segs[j].bytes) & 15) == 0;
+        }
+        a.vec16 = vec ? 1 : 0;
+        const size_t units = vec ? maxb / 16 : maxb / 4;
+        const unsigned gx = (unsigned)std::max<size_t>(1, std::min<size_t>(256, (units + 255) / 256));
+        hipLaunchKernelGGL(k_scatter_parts, dim3(gx, (unsigned)a.nseg), dim3(256), 0, st, a);
+        MHIP(m, hipGetLastError());
+        i = j;
+    }
+    return RT_OK;
+}
+/* Batch parameters shared by the roles. */
+struct BatchJob {
+    const rt_camera* cams = nullptr;  // kb cameras (equal sizes)
+    int kb = 0, bs = 0;
+    int32_t depth = 0, precision = 0, out_format = 0;
+    uint32_t flags = 0;
+};
+/* A sender's batch (a non-root rank; the root itself under RT_TRANSPORT_RCCL_LOOPBACK, self:
+ * render only, its send is in the root's group). */
+int batch_send(rt_multi* m, Rank* k, const BatchJob& b, bool self) {
+    const rt_camera& cam = b.cams[0];
+    const size_t row_bytes = (size_t)cam.width * bpp(b.out_format);
+    const Part pt = part_of(m, cam.height, k->rank);
+    const size_t bytes = (size_t)pt.nrows * row_bytes;
+    if (bytes == 0) return RT_OK;  // an empty band: nothing to render or send (the root posts none)
+    const size_t need = (size_t)b.kb * (size_t)max_part_rows(m, cam.height) * row_bytes;
+    if (need > k->bbuf_cap) {  // grow (rare): nothing in flight may use the old buffers
+        for (auto rs : k->render_stream) MHIP(m, hipStreamSynchronize(rs));
+        MHIP(m, hipStreamSynchronize(k->comm_stream));
+        for (auto& p : k->bbuf) {
+            if (p) MHIP(m, hipFree(p));
+            p = nullptr;
+        }
+        k->bbuf_cap = 0;
+        for (auto& p : k->bbuf) MHIP(m, hipMalloc(&p, need));
+        k->bbuf_cap = need;
+    }
+    hipStream_t rs = k->render_stream[b.bs];
+    MHIPF(m, hipStreamWaitEvent(rs, k->ev_bsent[b.bs], 0));  // this slot's last send is done
+    void* outs[RT_MULTI_BATCH_MAX];
+    for (int i = 0; i < b.kb; i++) outs[i] = static_cast<char*>(k->bbuf[b.bs]) + (size_t)i * bytes;
+    void* sts[1] = {rs};
+    {
+        SlowCall sc_("rt_render_device_frames (batch)");
+        const int e = rt_render_device_frames(k->ctx, b.cams, b.kb, pt.row0, pt.nrows, b.depth, b.precision,
+                                              b.flags, b.out_format, outs, b.kb, sts, 1, b.kb);
+        if (e != RT_OK) return ctx_err(m, k, e, "rt_render_device_frames (batch)");
+    }
+    MHIPF(m, hipEventRecord(k->ev_brend[b.bs], rs));
+    MHIPF(m, hipStreamWaitEvent(k->comm_stream, k->ev_brend[b.bs], 0));
+    if (self) return RT_OK;
+    m->queued.store(true, std::memory_order_relaxed);
+    const size_t total = (size_t)b.kb * bytes;
+    if (m->rccl()) {
+        MNCCL(m, ncclSend(k->bbuf[b.bs], total, ncclUint8, 0, k->comm, k->comm_stream));
+        MHIPF(m, hipEventRecord(k->ev_bsent[b.bs], k->comm_stream));
+        return RT_OK;
+    }
+    // THREADS: the mailbox's send, keyed by the batch's first frame
+    Post p;
+    int st = hub_take(m, &Hub::recv, m->frame, k->rank, &p, "waiting for the root's batch receive");
+    if (st != RT_OK) return st;
+    if (p.bytes != total) {
+        std::snprintf(m->last_err, sizeof m->last_err, "rank %d: the root expects %zu bytes, the batch has %zu",
+                      k->rank, p.bytes, total);
+        return RT_ERR_COMM;
+    }
+    MHIPF(m, hipStreamWaitEvent(k->comm_stream, p.ev, 0));
+    MHIPF(m, hipMemcpyPeerAsync(p.dst, p.device, k->bbuf[b.bs], k->device, total, k->comm_stream));
+    MHIPF(m, hipEventRecord(k->ev_bsent[b.bs], k->comm_stream));
+    Post done;
+    done.ev = k->ev_bsent[b.bs];
+    hub_put(m, &Hub::sent, m->frame, k->rank, done);
+    return RT_OK;
+}
+/* The root's batch: frames[i] / sts[i] = frame i's buffer and caller stream (distinct streams
+ * listed in uniq, at most RT_MULTI_SLOTS). */
+int batch_root(rt_multi* m, Rank* k, const BatchJob& b, char* const* frames, hipStream_t const* sts,
+               const std::vector<hipStream_t>& uniq) {
+    const rt_camera& cam = b.cams[0];
+    const size_t row_bytes = (size_t)cam.width * bpp(b.out_format);
+    const int N = m->nranks;
+    const bool lb = m->loopback();
+    // the scatter overwrites rows of frames that the caller's earlier work may still read
+    for (size_t u = 0; u < uniq.size(); u++) {
+        MHIPF(m, hipEventRecord(m->ev_in[u], uniq[u]));
+        MHIPF(m, hipStreamWaitEvent(k->comm_stream, m->ev_in[u], 0));
+    }
+    const Part p0 = part_of(m, cam.height, 0);
+    int st = RT_OK;
+    if (lb) {
+        st = batch_send(m, k, b, true);
+    } else if (p0.nrows > 0 && row_bytes > 0) {
+        void* outs[RT_MULTI_BATCH_MAX];
+        void* ss[RT_MULTI_BATCH_MAX];
+        for (int i = 0; i < b.kb; i++) {
+            outs[i] = frames[i] + (size_t)p0.row0 * row_bytes;
+            ss[i] = sts[i];
+        }
+        SlowCall sc_("rt_render_device_frames (root batch)");
+        const int e = rt_render_device_frames(k->ctx, b.cams, b.kb, p0.row0, p0.nrows, b.depth, b.precision,
+                                              b.flags, b.out_format, outs, b.kb, ss, b.kb, b.kb);
+        st = ctx_err(m, k, e, "rt_render_device_frames (root batch)");
+    }
+    if (st != RT_OK) return st;
+    // every sender's kb parts back to back in bstage[bs]
+    std::vector<size_t> off((size_t)N, 0), pb((size_t)N, 0);
+    std::vector<Part> parts((size_t)N);
+    size_t total = 0;
+    for (int g = lb ? 0 : 1; g < N; g++) {
+        parts[g] = part_of(m, cam.height, g);
+        pb[g] = (size_t)parts[g].nrows * row_bytes;
+        off[g] = total;
+        total += (size_t)b.kb * pb[g];
+    }
+    if (total == 0) {
+        MHIPF(m, hipEventRecord(k->ev_done, k->comm_stream));
+        return RT_OK;
+    }
+    if (total > k->bstage_cap) {  // grow (rare): the comm stream may still scatter from them
+        MHIP(m, hipStreamSynchronize(k->comm_stream));
+        for (auto& p : k->bstage) {
+            if (p) MHIP(m, hipFree(p));
+            p = nullptr;
+        }
+        k->bstage_cap = 0;
+        for (auto& p : k->bstage) MHIP(m, hipMalloc(&p, total));
+        k->bstage_cap = total;
+    }
+    char* stage = static_cast<char*>(k->bstage[b.bs]);
+    m->queued.store(true, std::memory_order_relaxed);
+    if (m->threads()) {
+        MHIPF(m, hipEventRecord(k->ev_ready[b.bs], k->comm_stream));
+        for (int g = 1; g < N; g++) {
+            if (pb[g] == 0) continue;
+            Post p;
+            p.dst = stage + off[g];
+            p.device = k->device;
+            p.bytes = (size_t)b.kb * pb[g];
+            p.ev = k->ev_ready[b.bs];
+            hub_put(m, &Hub::recv, m->frame, g, p);
+        }
+        for (int g = 1; g < N; g++) {
+            if (pb[g] == 0) continue;
+            Post p;
+            st = hub_take(m, &Hub::sent, m->frame, g, &p, "waiting for a batch's copy");
+            if (st != RT_OK) return st;
+            MHIPF(m, hipStreamWaitEvent(k->comm_stream, p.ev, 0));
+        }
+    } else {
+        MNCCL(m, ncclGroupStart());
+        for (int g = lb ? 0 : 1; g < N; g++) {
+            if (pb[g] == 0) continue;
+            ncclResult_t e = ncclSuccess;
+            if (g == 0) e = ncclSend(k->bbuf[b.bs], (size_t)b.kb * pb[0], ncclUint8, 0, k->comm, k->comm_stream);
+            if (e == ncclSuccess)
+                e = ncclRecv(stage + off[g], (size_t)b.kb * pb[g], ncclUint8, g, k->comm, k->comm_stream);
+            if (e != ncclSuccess) {
+                (void)ncclGroupEnd();
+                return nccl_err(m, e, "ncclRecv (batch)");
+            }
+        }
+        MNCCL(m, ncclGroupEnd());
+        if (m->fault_next) {  // RT_OPT_MULTI_FAULT (tests): fail once the gather is queued
+            m->fault_next = false;
+            std::snprintf(m->last_err, sizeof m->last_err, "injected fault after the gather was queued");
+            return RT_ERR_HIP;
+        }
+    }
+    std::vector<ScatterSeg> segs;
+    std::vector<int> fidx;
+    for (int i = 0; i < b.kb; i++)
+        for (int g = lb ? 0 : 1; g < N; g++) {
+            if (pb[g] == 0) continue;
+            segs.push_back({stage + off[g] + (size_t)i * pb[g], frames[i] + (size_t)parts[g].row0 * row_bytes,
+                            (uint64_t)pb[g]});
+            fidx.push_back(i);
+        }
+    st = scatter_segments(m, segs, fidx, frames, k->comm_stream);
+    if (st != RT_OK) return st;
+    MHIPF(m, hipEventRecord(k->ev_done, k->comm_stream));
+    if (lb) MHIPF(m, hipEventRecord(k->ev_bsent[b.bs], k->comm_stream));  // bbuf slot free again
+    return RT_OK;
+}
+
 void worker_main(rt_multi* m, Rank* k) {
     uint64_t seen = 0;
     for (;;) {
@@ -563,6 +815,12 @@ void destroy_rank(Rank* k, bool abort_comm) {
         if (k->ev_sent[s]) (void)hipEventDestroy(k->ev_sent[s]);
     }
     if (k->ev_done) (void)hipEventDestroy(k->ev_done);
+    for (int b = 0; b < 2; b++) {
+        if (k->ev_brend[b]) (void)hipEventDestroy(k->ev_brend[b]);
+        if (k->ev_bsent[b]) (void)hipEventDestroy(k->ev_bsent[b]);
+        if (k->bbuf[b]) (void)hipFree(k->bbuf[b]);
+        if (k->bstage[b]) (void)hipFree(k->bstage[b]);
+    }
     for (auto& e : k->ev_ready)
         if (e) (void)hipEventDestroy(e);
     for (auto& b : k->staging)
@@ -581,6 +839,79 @@ int check_args(const rt_multi* m, const rt_camera* cam, int32_t depth, int32_t p
     if (depth > rt_max_depth()) return RT_ERR_UNSUPPORTED;
     if (precision < RT_PREC_F64 || precision > RT_PREC_PATH64) return RT_ERR_INVALID_ARG;
     if (bpp(out_format) == 0) return RT_ERR_INVALID_ARG;
+    return RT_OK;
+}
+
+/* A frame (or batch) failed: out of step only if some rank already queued its part of the
+ * exchange (a failure before that — no scene, an unsupported combination — leaves the
+ * communicator usable); THREADS handles count frames in step, so any failure ends the
+ * exchange and wakes the peers' mailbox waits. */
+void mark_failed(rt_multi* m) {
+    if (m->threads()) {
+        m->broken = true;
+        hub_fail(m);
+    } else if (m->gathers() && m->queued.load(std::memory_order_relaxed)) {
+        m->broken = true;
+    }
+}
+
+/* rt_multi_render_device_frames in batches of m->batch frames (RT_OPT_MULTI_BATCH; the
+ * caller checked the arguments and that the batched exchange applies). */
+int render_batches(rt_multi* m, const rt_camera* cams, int32_t ncams, int32_t depth, int32_t precision,
+                   uint32_t flags, int32_t out_format, void* const* d_frames, int32_t nbufs,
+                   void* const* streams, int32_t nstreams, int32_t nframes) {
+    Rank* k = m->r[0];
+    DevGuard dg(k->device);
+    MHIP(m, dg.err);
+    const bool root = m->has_root();
+    std::vector<hipStream_t> uniq_all;
+    int last_bs = 0;
+    for (int32_t b0 = 0; b0 < nframes; b0 += m->batch) {
+        const int kb = (int)std::min<int32_t>(m->batch, nframes - b0);
+        rt_camera cb[RT_MULTI_BATCH_MAX];
+        for (int i = 0; i < kb; i++) cb[i] = cams[(b0 + i) % ncams];
+        BatchJob b;
+        b.cams = cb;
+        b.kb = kb;
+        b.bs = (int)(m->nbatch % 2);
+        b.depth = depth;
+        b.precision = precision;
+        b.flags = flags;
+        b.out_format = out_format;
+        m->queued.store(false, std::memory_order_relaxed);
+        int st;
+        if (root) {
+            char* fr[RT_MULTI_BATCH_MAX];
+            hipStream_t ss[RT_MULTI_BATCH_MAX];
+            std::vector<hipStream_t> uniq;
+            for (int i = 0; i < kb; i++) {
+                const int32_t f = b0 + i;
+                fr[i] = static_cast<char*>(d_frames[f % nbufs]);
+                void* cs = nstreams > 0 ? streams[f % nstreams] : nullptr;
+                ss[i] = cs ? static_cast<hipStream_t>(cs) : k->render_stream[f % m->slots];
+                if (std::find(uniq.begin(), uniq.end(), ss[i]) == uniq.end()) uniq.push_back(ss[i]);
+            }
+            st = batch_root(m, k, b, fr, ss, uniq);
+            for (hipStream_t u : uniq)
+                if (std::find(uniq_all.begin(), uniq_all.end(), u) == uniq_all.end()) uniq_all.push_back(u);
+        } else {
+            st = batch_send(m, k, b, false);
+        }
+        m->frame += (uint64_t)kb;
+        m->nbatch++;
+        if (st != RT_OK) {
+            mark_failed(m);
+            return st;
+        }
+        last_bs = b.bs;
+    }
+    // the caller's streams see the complete frames (root) / follow the last send
+    if (root) {
+        for (hipStream_t u : uniq_all) MHIPF(m, hipStreamWaitEvent(u, k->ev_done, 0));
+    } else {
+        for (int32_t s = 0; s < nstreams && s < nframes; s++)
+            if (streams[s]) MHIPF(m, hipStreamWaitEvent(static_cast<hipStream_t>(streams[s]), k->ev_bsent[last_bs], 0));
+    }
     return RT_OK;
 }
 
@@ -637,16 +968,7 @@ int render_frame(rt_multi* m, const rt_camera* cam, int32_t depth, int32_t preci
     }
     m->frame++;
     if (st != RT_OK) {
-        // out of step only if some rank already queued its part of the exchange (a failure
-        // before that — no scene, an unsupported combination — leaves the communicator
-        // usable); THREADS handles count frames in step, so any failure ends the exchange
-        // and wakes the peers' mailbox waits
-        if (m->threads()) {
-            m->broken = true;
-            hub_fail(m);
-        } else if (m->gathers() && m->queued.load(std::memory_order_relaxed)) {
-            m->broken = true;
-        }
+        mark_failed(m);
         return st;
     }
     if (root && (m->nranks > 1 || m->gathers())) {
@@ -738,6 +1060,11 @@ int rt_multi_create(const int32_t* devices, int32_t nlocal, int32_t nranks, int3
             if (e == hipSuccess) e = hipEventCreateWithFlags(&k->ev_ready[s], hipEventDisableTiming);
         }
         if (e == hipSuccess) e = hipEventCreateWithFlags(&k->ev_done, hipEventDisableTiming);
+        for (int b = 0; b < 2 && e == hipSuccess; b++) {
+            e = hipEventCreateWithFlags(&k->ev_brend[b], hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&k->ev_bsent[b], hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventRecord(k->ev_bsent[b], k->comm_stream);
+        }
         if (e != hipSuccess) fail(hip_err(m, e, "rank streams/events"));
     }
     if (st == RT_OK && m->has_root()) {
@@ -882,6 +1209,11 @@ int rt_multi_set_option(rt_multi* m, int32_t option, int64_t value) {
         m->slots = (int)value;
         return RT_OK;
     }
+    if (option == RT_OPT_MULTI_BATCH) {
+        if (value < 1 || value > RT_MULTI_BATCH_MAX) return RT_ERR_INVALID_ARG;
+        m->batch = (int)value;  // takes effect from the next rt_multi_render_device_frames
+        return RT_OK;
+    }
     if (option == RT_OPT_MULTI_LAYOUT) {
         if (value < 0 || value > 2) return RT_ERR_INVALID_ARG;
         const int st = rt_multi_sync(m);  // frames in flight keep the layout they started with
@@ -975,6 +1307,29 @@ int rt_multi_render_device_frames(rt_multi* m, const rt_camera* cams, int32_t nc
             m->frame += (uint64_t)nframes;
             return st;
         }
+    }
+    if (m->batch > 1 && nframes >= 2 && m->nlocal == 1 && m->gathers() && !m->broken &&
+        !(m->layout == 1 && m->nranks > 1)) {
+        // the batched exchange: every frame the same size (the bands are fixed per batch) and
+        // valid, at most RT_MULTI_SLOTS caller streams on the root (one ev_in each)
+        bool ok = true;
+        for (int32_t c = 0; c < ncams && c < nframes && ok; c++)
+            ok = cams[c].width == cams[0].width && cams[c].height == cams[0].height &&
+                 check_args(m, &cams[c], depth, precision, out_format) == RT_OK;
+        if (ok && m->has_root()) {
+            std::vector<void*> uniq;  // as render_batches picks them
+            for (int32_t f = 0; f < nframes && uniq.size() <= (size_t)RT_MULTI_SLOTS; f++) {
+                void* cs = nstreams > 0 ? streams[f % nstreams] : nullptr;
+                if (!cs) cs = m->r[0]->render_stream[f % m->slots];
+                if (std::find(uniq.begin(), uniq.end(), cs) == uniq.end()) uniq.push_back(cs);
+            }
+            ok = uniq.size() <= (size_t)RT_MULTI_SLOTS;
+            for (int32_t f = 0; f < nframes && f < nbufs && ok; f++)
+                ok = d_frames[f] != nullptr || (size_t)cams[0].width * cams[0].height == 0;
+        }
+        if (ok)
+            return render_batches(m, cams, ncams, depth, precision, flags, out_format, d_frames, nbufs,
+                                  streams, nstreams, nframes);
     }
     for (int32_t f = 0; f < nframes; f++) {
         const rt_camera* cam = &cams[f % ncams];

@@ -35,6 +35,7 @@ RT_TRANSPORT_RCCL_LOOPBACK = 2
 RT_TRANSPORT_THREADS = 3   # rehearsal: one handle per rank in one process (include/rt_capi.h)
 RT_MULTI_ID_BYTES = 128
 RT_MULTI_SLOTS = 4
+RT_MULTI_BATCH_MAX = 16
 
 RT_PRIM_SPHERE = 0
 RT_PRIM_WALL = 1
@@ -69,6 +70,7 @@ RT_OPT_MULTI_LAYOUT = 13
 RT_OPT_HOST_PIPELINE = 16
 RT_OPT_MULTI_FRAMES = 17
 RT_OPT_MULTI_FAULT = 18
+RT_OPT_MULTI_BATCH = 19
 RT_OPT_ROW_FEEDBACK_EMA = 14
 RT_OPT_ROW_FEEDBACK_ISOLATE = 15
 

@@ -295,6 +295,59 @@ def test_loopback_rccl_c4_full_size_frames_in_flight(rend):
             assert np.array_equal(b.cpu().numpy().view(np.uint32), ref.view(np.uint32))
 
 
+@pytest.mark.parametrize("fmt", [capi.RT_OUT_RGB_F32, capi.RT_OUT_RGBA8])
+def test_loopback_rccl_batched_gather(rend, fmt):
+    """RT_OPT_MULTI_BATCH through a real (one-rank) RCCL communicator: the root renders its
+    band of B frames back to back, sends them to itself in ONE ncclSend/ncclRecv pair into
+    its staging buffer and scatters them into the frames with the scatter kernel.  7 frames
+    of a moving camera over 2 buffers and 2 caller streams with B = 3 (batches 3, 3, 1) and
+    B = 16 (one batch): each buffer is bitwise the one-GPU frame of the last camera written
+    to it (the scatter keeps frame order when a batch revisits a buffer); then 9 frames of
+    one camera with B = 4 and the per-frame path (B = 1) on the same handle."""
+    import torch
+    dev = torch.device("cuda", 0)
+    cfg = scenes.CONFIGS["c2"]
+    prims = scenes.to_prims(cfg.scene())
+    rend.set_scene(prims)
+    W, H = cfg.width, cfg.height
+    cams = [_cam(W, H, 0.02 * k) for k in range(5)]
+    refs = [rend.render(c, 4, capi.RT_PREC_PATH64, 0, fmt)[0] for c in cams]
+    ch = 3 if fmt == capi.RT_OUT_RGB_F32 else 1
+    dt = torch.float32 if fmt == capi.RT_OUT_RGB_F32 else torch.int32
+    bufs = [torch.full((H, W, ch), -1, dtype=dt, device=dev) for _ in range(2)]
+    sts = [torch.cuda.Stream(dev) for _ in range(2)]
+    nf = 7
+    with capi.MultiRenderer([0], transport=capi.RT_TRANSPORT_RCCL_LOOPBACK) as m:
+        m.set_scene(prims)
+        for b in (3, 16):
+            m.set_option(capi.RT_OPT_MULTI_BATCH, b)
+            for x in bufs:
+                x.fill_(-1)
+            torch.cuda.synchronize()
+            m.render_device_frames(cams, 4, [x.data_ptr() for x in bufs], capi.RT_PREC_PATH64, 0, fmt,
+                                   streams=[s.cuda_stream for s in sts], nframes=nf)
+            torch.cuda.synchronize()
+            m.sync()
+            for i in range(2):
+                lf = max(f for f in range(nf) if f % 2 == i)
+                assert np.array_equal(bufs[i].cpu().numpy().view(np.uint32),
+                                      refs[lf % len(cams)].view(np.uint32)), (b, i)
+        for b in (4, 1):
+            m.set_option(capi.RT_OPT_MULTI_BATCH, b)
+            for x in bufs:
+                x.fill_(-1)
+            torch.cuda.synchronize()
+            m.render_device_frames([cams[0]], 4, [x.data_ptr() for x in bufs], capi.RT_PREC_PATH64, 0, fmt,
+                                   streams=[s.cuda_stream for s in sts], nframes=9)
+            torch.cuda.synchronize()
+            m.sync()
+            for x in bufs:
+                assert np.array_equal(x.cpu().numpy().view(np.uint32), refs[0].view(np.uint32)), b
+        for bad in (0, capi.RT_MULTI_BATCH_MAX + 1):
+            with pytest.raises(capi.RTError):
+                m.set_option(capi.RT_OPT_MULTI_BATCH, bad)
+
+
 def test_failure_before_the_gather_is_queued_keeps_the_communicator(rend):
     """A frame that fails before any rank queued its part of the gather (here: no scene
     yet, rejected before the root's loopback send/recv) returns its own status and leaves
@@ -369,8 +422,10 @@ def _run_threads(handles, fn):
     return errs
 
 
-@pytest.mark.parametrize("n,layout,frames", [(2, 0, 2), (3, 1, 2), (8, 1, 4), (4, 2, 3), (8, 2, 4)])
-def test_threads_transport_runs_the_process_per_gpu_branches(rend, n, layout, frames):
+@pytest.mark.parametrize("n,layout,frames,batch", [(2, 0, 2, 1), (3, 1, 2, 1), (8, 1, 4, 1), (4, 2, 3, 1),
+                                                  (8, 2, 4, 1), (2, 0, 2, 3), (4, 2, 3, 4), (8, 0, 4, 2),
+                                                  (8, 2, 4, 16), (3, 1, 2, 4)])
+def test_threads_transport_runs_the_process_per_gpu_branches(rend, n, layout, frames, batch):
     """RT_TRANSPORT_THREADS: n rt_multi handles in this process, one per rank (nlocal = 1,
     first_rank = r, one shared id), each driven from its own thread exactly as the
     process-per-GPU bench drives its rank — so the branches the first multi-GPU run takes
@@ -384,7 +439,12 @@ def test_threads_transport_runs_the_process_per_gpu_branches(rend, n, layout, fr
     flight over two root buffers, 2-4 band slots per rank (RT_OPT_MULTI_FRAMES): every buffer
     is bitwise the one-GPU frame of the last camera written to it, and a rank's band is
     already in the root's frame when its caller stream has passed the frame (checked on the
-    last frame)."""
+    last frame).  batch > 1 (RT_OPT_MULTI_BATCH): the batched exchange — each rank's bands of
+    `batch` frames in one send, the root's one receive per rank into staging and one scatter
+    kernel per run of distinct buffers (7 frames over 2 buffers: the frames land in order);
+    the interleaved layout keeps the per-frame exchange.  A batched rank's caller stream
+    follows its send (the part is in the root's staging; the frame rows come with the
+    root's scatter), so the per-rank snapshot applies to batch 1 only."""
     import os
     import torch
     dev = torch.device("cuda", 0)
@@ -409,6 +469,7 @@ def test_threads_transport_runs_the_process_per_gpu_branches(rend, n, layout, fr
             h.set_scene(prims)
             h.set_option(capi.RT_OPT_MULTI_LAYOUT, layout)
             h.set_option(capi.RT_OPT_MULTI_FRAMES, frames)
+            h.set_option(capi.RT_OPT_MULTI_BATCH, batch)
             if weights is not None:
                 h.set_row_weights(weights)
         torch.cuda.synchronize()
@@ -437,7 +498,7 @@ def test_threads_transport_runs_the_process_per_gpu_branches(rend, n, layout, fr
             got = bufs[b].cpu().numpy()
             assert np.array_equal(got.view(np.uint32), refs[lf % len(cams)].view(np.uint32)), (n, layout, b)
         ref_last = refs[last % len(cams)]
-        for r in range(1, n):
+        for r in range(1, n if batch == 1 or layout == 1 else 1):
             if layout == 1:
                 rows = capi.interleaved_row_index(H, n, r)
             elif layout == 2:
