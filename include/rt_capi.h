@@ -236,8 +236,14 @@ enum rt_option {
                                          the exchange (events, RCCL calls: ~20 us per frame,
                                          more than a 1/8 band's kernel) is paid once per B
                                          frames; a frame's rows reach the root when its batch
-                                         completes.  Every handle of one exchange must use the
-                                         same B and batch sizes.  The frames are identical. */
+                                         completes, and a non-root rank's caller stream
+                                         follows its batch's send.  A call batches when
+                                         B > 1, nframes >= 2 and every camera has the same
+                                         size (so every rank decides alike; every handle of
+                                         one exchange must use the same B); the root then
+                                         takes at most RT_MULTI_SLOTS distinct caller streams
+                                         (else RT_ERR_UNSUPPORTED).  The frames are
+                                         identical. */
     RT_OPT_MULTI_LAYOUT = 13,        /* rt_multi_set_option only: 0 (default) = contiguous
                                          row bands (rt_band_rows); 1 = interleaved tile rows
                                          (rt_interleaved_rows): balanced when the frame's cost

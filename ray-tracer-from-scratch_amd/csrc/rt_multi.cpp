@@ -1310,8 +1310,11 @@ int rt_multi_render_device_frames(rt_multi* m, const rt_camera* cams, int32_t nc
     }
     if (m->batch > 1 && nframes >= 2 && m->nlocal == 1 && m->gathers() && !m->broken &&
         !(m->layout == 1 && m->nranks > 1)) {
-        // the batched exchange: every frame the same size (the bands are fixed per batch) and
-        // valid, at most RT_MULTI_SLOTS caller streams on the root (one ev_in each)
+        // the batched exchange.  Whether a call batches must be the same on every rank (the
+        // root's receives match the senders' sends), so it depends only on what every rank
+        // is given alike: the option, the frame count, the cameras (every frame the same
+        // size, so the bands are fixed, and valid).  What only the root is given must then
+        // fit: at most RT_MULTI_SLOTS caller streams (one ev_in each), non-NULL buffers.
         bool ok = true;
         for (int32_t c = 0; c < ncams && c < nframes && ok; c++)
             ok = cams[c].width == cams[0].width && cams[c].height == cams[0].height &&
@@ -1323,9 +1326,15 @@ int rt_multi_render_device_frames(rt_multi* m, const rt_camera* cams, int32_t nc
                 if (!cs) cs = m->r[0]->render_stream[f % m->slots];
                 if (std::find(uniq.begin(), uniq.end(), cs) == uniq.end()) uniq.push_back(cs);
             }
-            ok = uniq.size() <= (size_t)RT_MULTI_SLOTS;
-            for (int32_t f = 0; f < nframes && f < nbufs && ok; f++)
-                ok = d_frames[f] != nullptr || (size_t)cams[0].width * cams[0].height == 0;
+            bool bufs = true;
+            for (int32_t f = 0; f < nframes && f < nbufs && bufs; f++)
+                bufs = d_frames[f] != nullptr || (size_t)cams[0].width * cams[0].height == 0;
+            if (uniq.size() > (size_t)RT_MULTI_SLOTS || !bufs) {
+                std::snprintf(m->last_err, sizeof m->last_err,
+                              "RT_OPT_MULTI_BATCH: the root takes at most %d distinct caller streams and "
+                              "non-NULL frame buffers", RT_MULTI_SLOTS);
+                return bufs ? RT_ERR_UNSUPPORTED : RT_ERR_INVALID_ARG;
+            }
         }
         if (ok)
             return render_batches(m, cams, ncams, depth, precision, flags, out_format, d_frames, nbufs,
