@@ -348,6 +348,60 @@ def test_loopback_rccl_batched_gather(rend, fmt):
                 m.set_option(capi.RT_OPT_MULTI_BATCH, bad)
 
 
+def test_batched_gather_ragged_empty_bands_and_root_limits(rend):
+    """RT_OPT_MULTI_BATCH with ranks that have no rows (a 5-row frame over 8 THREADS handles:
+    three empty bands, which post and send nothing) in RGBA8, batches 3 + 2 over one root
+    buffer: bitwise the one-GPU frame.  And the root-only limit: a batching call with more
+    than RT_MULTI_SLOTS distinct caller streams is refused (RT_ERR_UNSUPPORTED) before
+    anything is enqueued, and the handle stays usable."""
+    import os
+    import torch
+    dev = torch.device("cuda", 0)
+    W, H, n = 96, 5, 8
+    prims = scenes.to_prims(scenes.synthetic_scene(8, 4))
+    rend.set_scene(prims)
+    cams = [_cam(W, H, 0.03 * k) for k in range(5)]
+    fmt = capi.RT_OUT_RGBA8
+    refs = [rend.render(c, 4, capi.RT_PREC_PATH64, 0, fmt)[0] for c in cams]
+    uid = os.urandom(capi.RT_MULTI_ID_BYTES)
+    hs = [capi.MultiRenderer([0], nranks=n, first_rank=r, unique_id=uid,
+                             transport=capi.RT_TRANSPORT_THREADS) for r in range(n)]
+    buf = torch.full((H, W, 1), -1, dtype=torch.int32, device=dev)
+    sts = [torch.cuda.Stream(dev) for _ in range(n)]
+    try:
+        for h in hs:
+            h.set_scene(prims)
+            h.set_option(capi.RT_OPT_MULTI_BATCH, 3)
+        torch.cuda.synchronize()
+
+        def drive(r, h):
+            h.render_device_frames(cams, 4, [buf.data_ptr()] if r == 0 else [], capi.RT_PREC_PATH64, 0,
+                                   fmt, streams=[sts[r].cuda_stream], nframes=5)
+        errs = _run_threads(hs, drive)
+        assert errs == [None] * n, errs
+        torch.cuda.synchronize()
+        for h in hs:
+            h.sync()
+        assert np.array_equal(buf.cpu().numpy().view(np.uint32), refs[4].view(np.uint32))
+    finally:
+        for h in hs:
+            h.close()
+    with capi.MultiRenderer([0], transport=capi.RT_TRANSPORT_RCCL_LOOPBACK) as m:
+        m.set_scene(prims)
+        m.set_option(capi.RT_OPT_MULTI_BATCH, 2)
+        many = [torch.cuda.Stream(dev) for _ in range(capi.RT_MULTI_SLOTS + 1)]
+        bufs = [torch.full((H, W, 1), -1, dtype=torch.int32, device=dev) for _ in range(len(many))]
+        with pytest.raises(capi.RTError):
+            m.render_device_frames([cams[0]], 4, [b.data_ptr() for b in bufs], capi.RT_PREC_PATH64, 0, fmt,
+                                   streams=[s.cuda_stream for s in many], nframes=len(many))
+        m.render_device_frames([cams[0]], 4, [b.data_ptr() for b in bufs[:2]], capi.RT_PREC_PATH64, 0, fmt,
+                               streams=[s.cuda_stream for s in many[:2]], nframes=4)
+        torch.cuda.synchronize()
+        m.sync()
+        for b in bufs[:2]:
+            assert np.array_equal(b.cpu().numpy().view(np.uint32), refs[0].view(np.uint32))
+
+
 def test_failure_before_the_gather_is_queued_keeps_the_communicator(rend):
     """A frame that fails before any rank queued its part of the gather (here: no scene
     yet, rejected before the root's loopback send/recv) returns its own status and leaves
