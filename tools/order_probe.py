@@ -6,6 +6,9 @@ kernels compare scene indices on ties), so this prices a sphere permutation for 
 kernels' 64-sphere chunks before building one.
 
     python tools/order_probe.py c5
+
+Caveat: the orders are timed one after another on re-uploaded scenes, not interleaved; the
+built variant's interleaved A/B (tools/ab.py) disagreed with it.
 """
 import json, os, sys, ctypes as C
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
