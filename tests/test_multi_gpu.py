@@ -348,25 +348,27 @@ def test_loopback_rccl_batched_gather(rend, fmt):
                 m.set_option(capi.RT_OPT_MULTI_BATCH, bad)
 
 
-def test_batched_gather_ragged_empty_bands_and_root_limits(rend):
+@pytest.mark.parametrize("W,fmt", [(96, capi.RT_OUT_RGBA8), (97, capi.RT_OUT_RGB_F64)])
+def test_batched_gather_ragged_empty_bands_and_root_limits(rend, W, fmt):
     """RT_OPT_MULTI_BATCH with ranks that have no rows (a 5-row frame over 8 THREADS handles:
-    three empty bands, which post and send nothing) in RGBA8, batches 3 + 2 over one root
-    buffer: bitwise the one-GPU frame.  And the root-only limit: a batching call with more
-    than RT_MULTI_SLOTS distinct caller streams is refused (RT_ERR_UNSUPPORTED) before
-    anything is enqueued, and the handle stays usable."""
+    three empty bands, which post and send nothing), batches 3 + 2 over one root buffer, in
+    RGBA8 (16-byte scatter) and, 97 pixels wide, fp64 RGB (rows not a multiple of 16 bytes:
+    the 4-byte scatter): bitwise the one-GPU frame.  And the root-only limit: a batching
+    call with more than RT_MULTI_SLOTS distinct caller streams is refused
+    (RT_ERR_UNSUPPORTED) before anything is enqueued, and the handle stays usable."""
     import os
     import torch
     dev = torch.device("cuda", 0)
-    W, H, n = 96, 5, 8
+    H, n = 5, 8
     prims = scenes.to_prims(scenes.synthetic_scene(8, 4))
     rend.set_scene(prims)
     cams = [_cam(W, H, 0.03 * k) for k in range(5)]
-    fmt = capi.RT_OUT_RGBA8
     refs = [rend.render(c, 4, capi.RT_PREC_PATH64, 0, fmt)[0] for c in cams]
+    shape = (H, W, 1) if fmt == capi.RT_OUT_RGBA8 else (H, W, 6)
     uid = os.urandom(capi.RT_MULTI_ID_BYTES)
     hs = [capi.MultiRenderer([0], nranks=n, first_rank=r, unique_id=uid,
                              transport=capi.RT_TRANSPORT_THREADS) for r in range(n)]
-    buf = torch.full((H, W, 1), -1, dtype=torch.int32, device=dev)
+    buf = torch.full(shape, -1, dtype=torch.int32, device=dev)
     sts = [torch.cuda.Stream(dev) for _ in range(n)]
     try:
         for h in hs:
@@ -390,7 +392,7 @@ def test_batched_gather_ragged_empty_bands_and_root_limits(rend):
         m.set_scene(prims)
         m.set_option(capi.RT_OPT_MULTI_BATCH, 2)
         many = [torch.cuda.Stream(dev) for _ in range(capi.RT_MULTI_SLOTS + 1)]
-        bufs = [torch.full((H, W, 1), -1, dtype=torch.int32, device=dev) for _ in range(len(many))]
+        bufs = [torch.full(shape, -1, dtype=torch.int32, device=dev) for _ in range(len(many))]
         with pytest.raises(capi.RTError):
             m.render_device_frames([cams[0]], 4, [b.data_ptr() for b in bufs], capi.RT_PREC_PATH64, 0, fmt,
                                    streams=[s.cuda_stream for s in many], nframes=len(many))
