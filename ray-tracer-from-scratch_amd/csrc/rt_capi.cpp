@@ -604,19 +604,21 @@ rt::KParams make_params(const rt_ctx* ctx, const rt_camera* cam, int32_t row0, i
                         unsigned long long* d_segs, int32_t precision) {
     rt::KParams p{};
     const char* base = static_cast<const char*>(ctx->d_scene);
+    // section `off` of the device scene (null without one: rt_frame_boxes' host-only use)
+    auto at = [base](size_t off) -> const char* { return base ? base + off : nullptr; };
     p.s32 = reinterpret_cast<const rt::SphG32*>(base);
-    p.s64 = reinterpret_cast<const rt::SphG64*>(base + ctx->sc.off_s64);
-    p.w32 = reinterpret_cast<const rt::Wall32*>(base + ctx->sc.off_w32);
-    p.w64 = reinterpret_cast<const rt::Wall64*>(base + ctx->sc.off_w64);
-    p.sph_j = reinterpret_cast<const int32_t*>(base + ctx->sc.off_sj);
-    p.wall_j = reinterpret_cast<const int32_t*>(base + ctx->sc.off_wj);
-    p.mat = reinterpret_cast<const rt::DevMat*>(base + ctx->sc.off_mat);
-    p.mat32 = reinterpret_cast<const rt::DevMat32*>(base + ctx->sc.off_mat32);
-    p.wnn = reinterpret_cast<const double(*)[4]>(base + ctx->sc.off_wnn);
+    p.s64 = reinterpret_cast<const rt::SphG64*>(at(ctx->sc.off_s64));
+    p.w32 = reinterpret_cast<const rt::Wall32*>(at(ctx->sc.off_w32));
+    p.w64 = reinterpret_cast<const rt::Wall64*>(at(ctx->sc.off_w64));
+    p.sph_j = reinterpret_cast<const int32_t*>(at(ctx->sc.off_sj));
+    p.wall_j = reinterpret_cast<const int32_t*>(at(ctx->sc.off_wj));
+    p.mat = reinterpret_cast<const rt::DevMat*>(at(ctx->sc.off_mat));
+    p.mat32 = reinterpret_cast<const rt::DevMat32*>(at(ctx->sc.off_mat32));
+    p.wnn = reinterpret_cast<const double(*)[4]>(at(ctx->sc.off_wnn));
     const auto& cs = ctx->sc.cset[precision == RT_PREC_F32 ? 0 : 1];
-    p.clu = reinterpret_cast<const rt::Clu32*>(base + cs.off_clu);
-    p.csph = reinterpret_cast<const rt::CluSph*>(base + cs.off_csph);
-    p.cord = reinterpret_cast<const uint8_t*>(base + cs.off_cord);
+    p.clu = reinterpret_cast<const rt::Clu32*>(at(cs.off_clu));
+    p.csph = reinterpret_cast<const rt::CluSph*>(at(cs.off_csph));
+    p.cord = reinterpret_cast<const uint8_t*>(at(cs.off_cord));
     p.nclu = cs.nclu;
     p.clu_ls = cs.ls;
     p.clu_axis = cs.clu_axis;
