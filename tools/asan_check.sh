@@ -12,6 +12,7 @@ ASAN_RT=$(/opt/rocm/bin/hipcc -print-file-name=libclang_rt.asan-x86_64.so)
 for t in tests/test_bins_host.py tests/test_capi_host.py tests/test_cpp_dropin.py; do
   RT_AMD_LIB=$PWD/ray-tracer-from-scratch_amd/lib/asan/librt_amd.so LD_PRELOAD=$ASAN_RT \
   ASAN_OPTIONS=detect_leaks=0:halt_on_error=1 UBSAN_OPTIONS=print_stacktrace=1 \
-      python -m pytest "$t" -q -p no:cacheprovider -m "not gpu"
+      python -m pytest "$t" -q -p no:cacheprovider -m "not gpu" \
+      || { echo "asan_check: $t failed (rerun with ASAN_OPTIONS/UBSAN_OPTIONS log_path=... for the report)"; exit 1; }
 done
 echo "asan_check: clean"
