@@ -72,7 +72,13 @@ struct rt_ctx {
             int nclu = 0, clu_axis = 0, ls = 0;
             float clu_oinf = 0.0f;
         } cset[2];  // [0]: the F32 kernels' (CLU_SIZE), [1]: the fp64 kernels' (CLU_SIZE_D)
-        std::vector<char> bytes;    // the device image of the scene (rt_device.h layout)
+        // the device image of the scene (rt_device.h layout), built in 256-byte aligned host
+        // memory so its records (alignas 32-128) may be written through their own types
+        struct alignas(256) Blk {
+            char b[256];
+        };
+        std::vector<Blk> blocks;
+        char* image() { return reinterpret_cast<char*>(blocks.data()); }
         std::vector<double> h_sph;  // nS x {cx, cy, cz, radius^2, radius}
         std::vector<double> h_wal;  // nW x {P, n, X, Y, length, width}
         std::vector<double> h_km;   // metallic of each material slot
@@ -864,9 +870,12 @@ int pack_scene(const rt_prim* prims, int32_t n, rt_ctx::SceneHost& sc) {
         off = align_up(cs.off_cord + 8 * rt::CLU_MAX, 256);
     }
     const size_t total = off + 256;
-    sc.bytes.assign(total, 0);
+    sc.blocks.assign((total + 255) / 256, {});
     sc.total = total;
-    std::vector<char>& host = sc.bytes;
+    struct {
+        char* p;
+        char* data() { return p; }
+    } host{sc.image()};
     auto* s32 = reinterpret_cast<rt::SphG32*>(host.data());
     auto* s64 = reinterpret_cast<rt::SphG64*>(host.data() + off_s64);
     auto* w32 = reinterpret_cast<rt::Wall32*>(host.data() + off_w32);
@@ -1187,7 +1196,7 @@ int rt_set_scene(rt_ctx* ctx, const rt_prim* prims, int32_t n) {
         RT_HIP(ctx, hipMalloc(&ctx->d_scene, sc.total));
         ctx->scene_bytes = sc.total;
     }
-    RT_HIP(ctx, hipMemcpy(ctx->d_scene, sc.bytes.data(), sc.total, hipMemcpyHostToDevice));
+    RT_HIP(ctx, hipMemcpy(ctx->d_scene, sc.image(), sc.total, hipMemcpyHostToDevice));
     ctx->sc = std::move(sc);
     ctx->have_scene = true;
     ctx->scene_gen++;
