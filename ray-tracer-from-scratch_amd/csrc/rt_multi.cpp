@@ -95,7 +95,7 @@ struct Rank {
     size_t bbuf_cap = 0;
     void* bstage[2] = {};
     size_t bstage_cap = 0;
-    hipEvent_t ev_brend[2] = {}, ev_bsent[2] = {};
+    hipEvent_t ev_brend[2][RT_MULTI_SLOTS] = {}, ev_bsent[2] = {};
     // worker thread (local ranks other than the first, one process driving several GPUs)
     std::thread th;
     std::mutex mu;
@@ -625,19 +625,27 @@ int batch_send(rt_multi* m, Rank* k, const BatchJob& b, bool self) {
         for (auto& p : k->bbuf) MHIP(m, hipMalloc(&p, need));
         k->bbuf_cap = need;
     }
-    hipStream_t rs = k->render_stream[b.bs];
-    MHIPF(m, hipStreamWaitEvent(rs, k->ev_bsent[b.bs], 0));  // this slot's last send is done
+    // the batch's frames round-robin over RT_OPT_MULTI_FRAMES render streams, so a small
+    // band's long last waves overlap the next frames' (one stream would run them one after
+    // another), each stream first waiting until this slot's last send is done
+    const int S = std::max(1, std::min(m->slots, b.kb));
+    void* sts[RT_MULTI_SLOTS];
+    for (int j = 0; j < S; j++) {
+        sts[j] = k->render_stream[j];
+        MHIPF(m, hipStreamWaitEvent(k->render_stream[j], k->ev_bsent[b.bs], 0));
+    }
     void* outs[RT_MULTI_BATCH_MAX];
     for (int i = 0; i < b.kb; i++) outs[i] = static_cast<char*>(k->bbuf[b.bs]) + (size_t)i * bytes;
-    void* sts[1] = {rs};
     {
         SlowCall sc_("rt_render_device_frames (batch)");
         const int e = rt_render_device_frames(k->ctx, b.cams, b.kb, pt.row0, pt.nrows, b.depth, b.precision,
-                                              b.flags, b.out_format, outs, b.kb, sts, 1, b.kb);
+                                              b.flags, b.out_format, outs, b.kb, sts, S, b.kb);
         if (e != RT_OK) return ctx_err(m, k, e, "rt_render_device_frames (batch)");
     }
-    MHIPF(m, hipEventRecord(k->ev_brend[b.bs], rs));
-    MHIPF(m, hipStreamWaitEvent(k->comm_stream, k->ev_brend[b.bs], 0));
+    for (int j = 0; j < S; j++) {  // the send follows every stream's frames
+        MHIPF(m, hipEventRecord(k->ev_brend[b.bs][j], k->render_stream[j]));
+        MHIPF(m, hipStreamWaitEvent(k->comm_stream, k->ev_brend[b.bs][j], 0));
+    }
     if (self) return RT_OK;
     m->queued.store(true, std::memory_order_relaxed);
     const size_t total = (size_t)b.kb * bytes;
@@ -816,7 +824,8 @@ void destroy_rank(Rank* k, bool abort_comm) {
     }
     if (k->ev_done) (void)hipEventDestroy(k->ev_done);
     for (int b = 0; b < 2; b++) {
-        if (k->ev_brend[b]) (void)hipEventDestroy(k->ev_brend[b]);
+        for (auto e : k->ev_brend[b])
+            if (e) (void)hipEventDestroy(e);
         if (k->ev_bsent[b]) (void)hipEventDestroy(k->ev_bsent[b]);
         if (k->bbuf[b]) (void)hipFree(k->bbuf[b]);
         if (k->bstage[b]) (void)hipFree(k->bstage[b]);
@@ -1061,7 +1070,8 @@ int rt_multi_create(const int32_t* devices, int32_t nlocal, int32_t nranks, int3
         }
         if (e == hipSuccess) e = hipEventCreateWithFlags(&k->ev_done, hipEventDisableTiming);
         for (int b = 0; b < 2 && e == hipSuccess; b++) {
-            e = hipEventCreateWithFlags(&k->ev_brend[b], hipEventDisableTiming);
+            for (int j = 0; j < RT_MULTI_SLOTS && e == hipSuccess; j++)
+                e = hipEventCreateWithFlags(&k->ev_brend[b][j], hipEventDisableTiming);
             if (e == hipSuccess) e = hipEventCreateWithFlags(&k->ev_bsent[b], hipEventDisableTiming);
             if (e == hipSuccess) e = hipEventRecord(k->ev_bsent[b], k->comm_stream);
         }
