@@ -89,8 +89,8 @@ struct Rank {
     void* staging[RT_MULTI_SLOTS] = {};
     size_t staging_cap = 0;
     // batched gather (RT_OPT_MULTI_BATCH), two batch slots: a sender's bands of the batch's
-    // frames back to back (bbuf), the root's received parts (bstage); ev_brend: the batch's
-    // bands rendered, ev_bsent: its send complete (bbuf free again)
+    // frames back to back (bbuf), the root's received parts (bstage); ev_brend[slot][j]: the
+    // batch's bands on render stream j rendered, ev_bsent: its send complete (bbuf free again)
     void* bbuf[2] = {};
     size_t bbuf_cap = 0;
     void* bstage[2] = {};
@@ -533,8 +533,8 @@ int enqueue_rank(rt_multi* m, Rank* k, const Job& j) {
 
 /* ---- batched gather (RT_OPT_MULTI_BATCH) ----
  * A batch of kb frames is one exchange: every sender renders its band of the kb frames back
- * to back into bbuf (the ctx's own frame loop, with its host pipeline, on one render stream)
- * and sends the kb bands in ONE ncclSend; the root renders its rows of the kb frames in place
+ * to back into bbuf (the ctx's own frame loop, with its host pipeline, round-robin over its
+ * render streams) and sends the kb bands in ONE ncclSend; the root renders its rows of the kb frames in place
  * on the caller's streams, receives every rank's kb bands into bstage in ONE group, and
  * copies them into the frames' rows with one scatter kernel.  Two batch slots: batch b + 1
  * renders while batch b is in flight.  Per frame that is one launch plus 1/kb of the
