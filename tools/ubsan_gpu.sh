@@ -3,7 +3,8 @@
 # lib/ubsan/librt_amd.so (`make ubsan`: UndefinedBehaviorSanitizer on the C-ABI's host code,
 # rt_capi.cpp and rt_multi.cpp — the multi-GPU exchange, the host pipeline — with the device
 # code unchanged; the UBSan runtime is a dependency of the library, nothing is preloaded).
-# Any report aborts the test process (-fno-sanitize-recover).  Build it beforehand, here.
+# Any report aborts the test process (-fno-sanitize-recover).  Build it beforehand, here, and
+# take its line out of .gpurunignore for the run (it is listed there to keep pushes small).
 set -eu
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 LIB=$PWD/ray-tracer-from-scratch_amd/lib/ubsan/librt_amd.so
