@@ -30,6 +30,16 @@ kernel time; the frame-sharded side run (N > 1); the CPU baseline (rank 0, N = 1
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2] [--precision mixed]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+Process model: one process per GPU.  Under a launcher (torch.distributed.run: RANK /
+WORLD_SIZE / LOCAL_RANK / MASTER_* in the environment) every process is one rank.  Without
+one, `--gpus N` > 1 makes this process a supervisor: it starts N child processes of this
+script (one per rank, RANK = LOCAL_RANK = r, MASTER_ADDR 127.0.0.1, a free port,
+GPU_MAX_HW_QUEUES=16) before anything touches the GPU, forwards rank 0's JSON line, and if
+any child exits non-zero or the --deadline passes it stops the others and exits non-zero
+naming the rank.  Every rank also has its own deadline watchdog.  `--transport ipc` runs
+the row-tiled operator's process-per-GPU code across processes on ONE GPU
+(RT_TRANSPORT_IPC, a rehearsal: torch.distributed over gloo, the gather through HIP IPC).
 """
 from __future__ import annotations
 
@@ -133,12 +143,103 @@ def load_profile(path: str, workload: str, precision: str):
         return None
 
 
-def main() -> int:
-    # stdout carries the ONE JSON line: anything the libraries print there (RCCL's version
-    # banner when a communicator is made) goes to stderr, the JSON to a private copy of fd 1
+def free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def supervise(args, argv) -> int:
+    """`--gpus N` > 1 without a launcher: N child processes of this script, one per rank,
+    started before anything here touches the GPU (no torch.cuda, no librt_amd.so in this
+    process).  Rank 0's stdout (its one JSON line) is forwarded; the other ranks' stdout goes
+    to stderr.  A child exiting non-zero or the deadline passing stops every other child
+    (SIGTERM, then SIGKILL) and exits non-zero with the rank named."""
+    import signal
+    import subprocess
+    import threading
+    n = args.gpus
+    port = free_port()
+    script = os.path.abspath(__file__)
+    procs, lines = [], []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        env.setdefault("GPU_MAX_HW_QUEUES", "16")
+        procs.append(subprocess.Popen([sys.executable, "-u", script] + argv, env=env,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno()))
+
+    def pump():
+        for ln in procs[0].stdout:
+            lines.append(ln.decode(errors="replace"))
+
+    th = threading.Thread(target=pump, daemon=True)
+    th.start()
+    t0 = time.monotonic()
+    beat = t0
+    failed = None
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+        if bad:
+            failed = f"rank {bad[0][0]} exited with status {bad[0][1]}"
+            break
+        if all(c == 0 for c in codes):
+            break
+        now = time.monotonic()
+        if now - t0 > args.deadline:
+            late = [r for r, c in enumerate(codes) if c is None]
+            failed = f"deadline {args.deadline:.0f} s passed with rank(s) {late} still running"
+            break
+        if now - beat > 60:
+            beat = now
+            print(f"bench supervisor: {n} ranks running for {now - t0:.0f} s", file=sys.stderr,
+                  flush=True)
+        time.sleep(0.05)
+    if failed:
+        print(f"bench supervisor: {failed}; stopping the other ranks", file=sys.stderr, flush=True)
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(signal.SIGTERM)
+        t1 = time.monotonic()
+        while any(p.poll() is None for p in procs) and time.monotonic() - t1 < 10:
+            time.sleep(0.05)
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+        for p in procs:
+            p.wait()
+        th.join(5)
+        return 3
+    th.join(10)
+    for ln in lines:
+        sys.stdout.write(ln)
     sys.stdout.flush()
-    json_out = os.fdopen(os.dup(1), "w")
-    os.dup2(2, 1)
+    return 0
+
+
+PHASE = ["start"]
+
+
+def start_watchdog(seconds: float, rank: int) -> None:
+    """Ends this rank's process (status 124) if it is still running after `seconds`: a peer
+    rank that failed leaves this one blocked in a collective or a stream wait that never
+    completes, which must become an exit naming the rank, not a silent hang."""
+    import threading
+
+    def fire():
+        print(f"bench rank {rank}: deadline {seconds:.0f} s passed in phase '{PHASE[0]}'",
+              file=sys.stderr, flush=True)
+        os._exit(124)
+
+    t = threading.Timer(seconds, fire)
+    t.daemon = True
+    t.start()
+
+
+def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawTextHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -158,8 +259,11 @@ def main() -> int:
     ap.add_argument("--tiler", default="native", choices=["native", "torch"],
                     help="tiled mode: the C-ABI's rt_multi (RCCL send/recv in C++), or "
                          "rtamd.tiling over torch.distributed")
-    ap.add_argument("--transport", default="rccl", choices=["rccl", "copy"],
-                    help="rt_multi transport (copy: one process only, --local-ranks)")
+    ap.add_argument("--transport", default="rccl", choices=["rccl", "copy", "ipc"],
+                    help="rt_multi transport: rccl (the product), copy (one process only, "
+                         "--local-ranks), ipc (one process per rank on any number of GPUs, "
+                         "HIP IPC + a shared-memory mailbox: the rehearsal of the "
+                         "process-per-GPU path on one GPU; torch.distributed over gloo)")
     ap.add_argument("--band-layout", default="weighted", choices=["equal", "weighted"],
                     help="tiled mode, N > 1: rank r's rows of the frame — equal contiguous bands "
                          "(rt_band_rows), or contiguous bands cut so each carries 1/N of the "
@@ -194,23 +298,42 @@ def main() -> int:
     ap.add_argument("--box-cache", type=int, default=0, choices=[0, 1],
                     help="RT_OPT_BOX_CACHE: reuse the host's per-frame pixel boxes when the "
                          "camera is unchanged (0 = recompute every frame)")
+    ap.add_argument("--deadline", type=float, default=900.0,
+                    help="seconds: the supervisor (and each rank's watchdog) ends the run "
+                         "non-zero if it is still going")
+    ap.add_argument("--fault-rank", type=int, default=-1,
+                    help="test hook: this rank's frame right after the gather check fails "
+                         "(RT_OPT_MULTI_FAULT) — every rank must then exit non-zero")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     ap.add_argument("--valu-json", default=os.path.join(REPO, "profiles", "pmc_valu.json"))
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
 
-    import torch
-    import torch.distributed as dist
-
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return supervise(args, sys.argv[1:] if argv is None else list(argv))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    # RT_BENCH_BACKEND=gloo: rehearsal of the N-rank code path on fewer GPUs than ranks
-    # (ranks share devices round-robin; RCCL refuses two ranks on one GPU, so the tiled mode
-    # then uses the torch tiler over gloo).  Not a measurement: the driver's multi-GPU runs
-    # use the default, RCCL ("nccl").
-    backend = os.environ.get("RT_BENCH_BACKEND", "nccl")
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE {world} (launch N ranks with --gpus N)",
+              file=sys.stderr)
+        return 2
+    start_watchdog(args.deadline, rank)
+
+    # stdout carries the ONE JSON line: anything the libraries print there (RCCL's version
+    # banner when a communicator is made) goes to stderr, the JSON to a private copy of fd 1
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+
+    import torch
+    import torch.distributed as dist
+
+    # RT_BENCH_BACKEND=gloo (or --transport ipc): rehearsal of the N-rank code path on fewer
+    # GPUs than ranks (ranks share devices round-robin; RCCL refuses two ranks on one GPU, so
+    # the tiled mode then uses the torch tiler over gloo, or with --transport ipc the native
+    # operator over HIP IPC).  Not a measurement: the driver's multi-GPU runs use the
+    # default, RCCL ("nccl").
+    backend = os.environ.get("RT_BENCH_BACKEND", "gloo" if args.transport == "ipc" else "nccl")
     if backend == "gloo":
         local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
@@ -234,7 +357,9 @@ def main() -> int:
     flags = capi.RT_FLAG_SUN if args.sun else 0
     depth = cfg.depth
     tiled_mode = args.mode == "tiled"
-    tiler = args.tiler if not (tiled_mode and world > 1 and backend == "gloo") else "torch"
+    tiler = args.tiler if not (tiled_mode and world > 1 and backend == "gloo"
+                               and args.transport != "ipc") else "torch"
+    PHASE[0] = "setup"
 
     rend = capi.Renderer(local)   # census, side measurements, frames mode, kernel time
     rend.set_option(capi.RT_OPT_BOX_CACHE, args.box_cache)
@@ -273,16 +398,24 @@ def main() -> int:
     stream = streams[0]
     torch.cuda.set_stream(stream)
     st_ptrs = [s_.cuda_stream for s_ in streams]
+    rank_batch = max(1, min(capi.RT_MULTI_BATCH_MAX, args.rank_batch))
     # frame buffers: the whole frame on rank 0 (tiled: the bands are gathered into it) or on
-    # every rank (frames mode); fp32-RGB sized, which the sweep below also writes
+    # every rank (frames mode); fp32-RGB sized, which the sweep below also writes.  The
+    # batched exchange (N > 1) needs a distinct buffer per frame of a batch (rt_capi.h
+    # RT_OPT_MULTI_BATCH): 2 x B of them, so consecutive batches never share one and every
+    # frame is whole in its buffer
     full = (not tiled_mode) or rank == 0
+    nbuf = fif
+    if tiled_mode and tiler == "native" and (world > 1 or args.local_ranks > 1) and full:
+        nbuf = max(fif, 2 * rank_batch)
     outs = [torch.empty((H if full else max(1, nrows), W, 3), dtype=torch.float32, device=dev)
-            for _ in range(fif)]
+            for _ in range(nbuf)]
     out = outs[0]
     out_ptrs = [o.data_ptr() for o in outs]
     segs_t = torch.zeros(1, dtype=torch.int64, device=dev)
 
     # ---- census: exact segment count of this rank's rows (untimed) ----
+    PHASE[0] = "census"
     rend.render_device(cam, depth, out.data_ptr(), prec, flags, capi.RT_OUT_RGB_F32, row0=row0,
                        nrows=nrows, d_segments=segs_t.data_ptr(), stream=stream.cuda_stream)
     torch.cuda.synchronize(dev)
@@ -294,10 +427,17 @@ def main() -> int:
     frame_segs = total_segs if tiled_mode else my_segs   # one frame
 
     # ---- the tiled frame operator ----
+    PHASE[0] = "operator setup"
     multi = None
     torch_tiled = None
     if tiled_mode and tiler == "native":
-        if world > 1:
+        if world > 1 and args.transport == "ipc":
+            # any shared bytes name the IPC mailbox: rank 0's random id, broadcast
+            uid = [os.urandom(capi.RT_MULTI_ID_BYTES) if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            multi = capi.MultiRenderer([local], nranks=world, first_rank=rank, unique_id=uid[0],
+                                       transport=capi.RT_TRANSPORT_IPC)
+        elif world > 1:
             uid = [capi.multi_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(uid, src=0)
             multi = capi.MultiRenderer([local], nranks=world, first_rank=rank, unique_id=uid[0])
@@ -308,26 +448,29 @@ def main() -> int:
             multi = capi.MultiRenderer([local])
         multi.set_option(capi.RT_OPT_BOX_CACHE, args.box_cache)
         multi.set_option(capi.RT_OPT_ROW_FEEDBACK, args.row_feedback)
+        multi.set_option(capi.RT_OPT_MULTI_TIMEOUT_MS, int(args.deadline * 1000))
         multi.set_scene(prims)
         if layout == 2:
             multi.set_row_weights(weights)
         multi.set_option(capi.RT_OPT_MULTI_LAYOUT, layout)
         if multi.nranks > 1:
             multi.set_option(capi.RT_OPT_MULTI_FRAMES, max(1, min(capi.RT_MULTI_SLOTS, args.rank_frames)))
-            multi.set_option(capi.RT_OPT_MULTI_BATCH, max(1, min(capi.RT_MULTI_BATCH_MAX, args.rank_batch)))
+            multi.set_option(capi.RT_OPT_MULTI_BATCH, rank_batch)
     elif tiled_mode:
         from rtamd import tiling
         # double-buffered: the gather of frame k (collective stream) overlaps the render of k+1
-        band_max = -(-H // world)
-        band_bufs = [torch.empty((band_max, W, ch), dtype=tdt, device=dev)]
         torch_tiled = tiling.TiledFrames(
             lambda r0, n, buf: rend.render_device(cam, depth, buf.data_ptr(), prec, flags, out_fmt,
                                                   row0=r0, nrows=n, stream=stream.cuda_stream),
             H, W, ch, tdt, dev, depth=2)
-        del band_bufs
+    n_ranks = multi.nranks if multi is not None else world
 
-    # ---- the gathered frame against rank 0's own one-GPU render of the same frame, bitwise
-    # (untimed): the row-tiled operator must only move bytes (pixels are independent) ----
+    # ---- the gathered frames against rank 0's own one-GPU render of the same frame, bitwise
+    # (untimed): the row-tiled operator must only move bytes (pixels are independent).  Both
+    # exchanges the operator has: the batched one (3 batches of B frames over 2 B buffers,
+    # so the third batch renders into the first one's buffers) and the per-frame one (3
+    # frames over 2 buffers); EVERY buffer is compared ----
+    PHASE[0] = "gather check"
     gather_check = None
     if tiled_mode:
         ref = None
@@ -336,41 +479,56 @@ def main() -> int:
             ref = torch.empty((H, W, ch), dtype=tdt, device=dev)
             rend.render_device(cam, depth, ref.data_ptr(), prec, flags, out_fmt,
                                stream=stream.cuda_stream)
-        got = None
         chk = multi
         op_name = None
         if multi is not None and world == 1 and multi.nranks == 1:
             # one GPU: the timed operator renders the frame in place (no communicator); check
             # the gather's RCCL calls here instead, untimed, through a one-rank loopback
             # communicator (the root's band sent to itself: ncclCommInitRank, the group,
-            # ncclSend/ncclRecv, ncclCommGetAsyncError all run)
+            # ncclSend/ncclRecv, ncclCommGetAsyncError all run), batched as N > 1 runs are
             chk = capi.MultiRenderer([local], transport=capi.RT_TRANSPORT_RCCL_LOOPBACK)
             chk.set_option(capi.RT_OPT_ROW_FEEDBACK, args.row_feedback)
-            # the batched exchange the N > 1 runs use (its three frames in one batch)
-            chk.set_option(capi.RT_OPT_MULTI_BATCH, max(1, min(capi.RT_MULTI_BATCH_MAX, args.rank_batch)))
             chk.set_scene(prims)
             op_name = ("rt_multi, RT_TRANSPORT_RCCL_LOOPBACK: RCCL send/recv of the one band "
-                       "through a one-rank communicator, batched as the N > 1 runs are "
-                       f"(RT_OPT_MULTI_BATCH {args.rank_batch}; the timed N = 1 loop renders in place)")
+                       "through a one-rank communicator (the timed N = 1 loop renders in place)")
         elif multi is not None:
             op_name = (f"rt_multi, {multi.nranks} ranks, "
-                       + ("RCCL send/recv" if args.transport == "rccl" and world > 1
-                          else "peer copies (rehearsal)")
-                       + f", {args.band_layout} bands"
-                       + (f", {args.rank_batch} frames per gather" if world > 1 else ""))
+                       + {"rccl": "RCCL send/recv", "ipc": "HIP IPC copies between processes "
+                          "(rehearsal)", "copy": "peer copies (rehearsal)"}[
+                           args.transport if world > 1 else "copy"]
+                       + f", {args.band_layout} bands")
+        checks = {}
         if chk is not None:
-            outs[0].fill_(-1.0)
-            torch.cuda.synchronize(dev)
-            # three frames in flight over two buffers: buffer 0 ends with the third
-            chk.render_device_frames([cam], depth, out_ptrs[:2] if chk.has_root else [], prec,
-                                     flags, out_fmt, streams=st_ptrs[:2] if chk.has_root else st_ptrs[:1],
-                                     nframes=3 if len(out_ptrs) > 1 else 1)
-            torch.cuda.synchronize(dev)
-            chk.sync()
-            if rank == 0:
-                got = outs[0].view(torch.uint8).flatten()[:nbytes]
+            nb = 2 * rank_batch
+            cbufs = ([torch.empty((H, W, ch), dtype=tdt, device=dev) for _ in range(nb)]
+                     if rank == 0 else [])
+            cptrs = [b_.data_ptr() for b_ in cbufs]
+            cases = [("batched", rank_batch, nb, 3 * rank_batch), ("per_frame", 1, 2, 3)]
+            for name, bsz, nbs, nfr in cases:
+                if name == "batched" and bsz == 1:
+                    continue
+                chk.set_option(capi.RT_OPT_MULTI_BATCH, bsz)
+                for b_ in cbufs:
+                    b_.fill_(255 if tdt == torch.uint8 else -1.0)
+                torch.cuda.synchronize(dev)
+                chk.render_device_frames([cam], depth, cptrs[:nbs] if chk.has_root else [], prec,
+                                         flags, out_fmt,
+                                         streams=st_ptrs[:2] if chk.has_root else st_ptrs[:1],
+                                         nframes=nfr)
+                torch.cuda.synchronize(dev)
+                chk.sync()
+                barrier()
+                if rank == 0:
+                    rb = ref.view(torch.uint8).flatten()[:nbytes]
+                    eqs = [bool(torch.equal(b_.view(torch.uint8).flatten()[:nbytes], rb))
+                           for b_ in cbufs[:nbs]]
+                    checks[name] = {"frames": nfr, "buffers": nbs, "frames_per_gather": bsz,
+                                    "every_buffer_bitwise_equal": all(eqs)}
+            if multi is not None and multi.nranks > 1:
+                chk.set_option(capi.RT_OPT_MULTI_BATCH, rank_batch)
             if chk is not multi:
                 chk.close()
+            del cbufs
         elif torch_tiled is not None:
             h_ = torch_tiled.submit()
             torch_tiled.wait(h_)
@@ -378,17 +536,25 @@ def main() -> int:
             torch.cuda.synchronize(dev)
             if rank == 0:
                 got = torch_tiled.frame(h_[0]).view(torch.uint8).flatten()[:nbytes]
+                checks["per_frame"] = {"frames": 1, "every_buffer_bitwise_equal":
+                                       bool(torch.equal(got, ref.view(torch.uint8).flatten()[:nbytes]))}
+                del got
         barrier()
         if rank == 0:
-            eq = bool(torch.equal(got, ref.view(torch.uint8).flatten()[:nbytes]))
-            gather_check = {"bitwise_equal_to_one_gpu_frame": eq, "ranks": world,
-                            "output": args.out,
+            eq = bool(checks) and all(c["every_buffer_bitwise_equal"] for c in checks.values())
+            gather_check = {"bitwise_equal_to_one_gpu_frame": eq, "ranks": n_ranks,
+                            "output": args.out, **checks,
                             "operator": op_name if multi is not None
                             else "rtamd.tiling (torch.distributed gather)"}
             if not eq:
-                print(f"bench: the gathered {world}-rank frame differs from the one-GPU frame",
+                print(f"bench: a gathered {n_ranks}-rank frame differs from the one-GPU frame",
                       file=sys.stderr)
-            del ref, got
+            del ref
+
+    if args.fault_rank == rank and multi is not None:
+        # test hook: this rank's next frame fails once its part of the exchange is queued
+        multi.set_option(capi.RT_OPT_MULTI_FAULT, 1)
+        print(f"bench rank {rank}: injecting a fault into the next frame", file=sys.stderr)
 
     def run_steps(n: int):
         """n consecutive frames, enqueued by ONE C-ABI call (or the torch tiler's loop)."""
@@ -514,6 +680,7 @@ def main() -> int:
     # runs 20 steps) spends its first frames on the order's ramp-up (measured: 20-step
     # regions 33-40 us/frame vs 29 over 200 frames) ----
     steady = None
+    PHASE[0] = "steady state"
     if not args.no_sweep:
         nst = max(1, args.steady_frames)
         torch.cuda.synchronize(dev)
@@ -570,6 +737,7 @@ def main() -> int:
                    "mrays_per_s_median": round(total_segs / (q[len(q) // 2] * 1e-3) / 1e6, 1)}
 
     # ---- warmup + timed region ----
+    PHASE[0] = "timed region"
     run_steps(args.warmup)
     hot_sync()
     if multi is not None:
@@ -618,6 +786,7 @@ def main() -> int:
 
     # ---- N > 1 side run: the weak (frame-sharded) layout, same frame loop, no collective --
     sharded = None
+    PHASE[0] = "side runs"
     if tiled_mode and world > 1 and not args.no_sweep:
         # whole frames on every rank: full-size buffers (a non-root rank's `outs` hold a band)
         if full:
@@ -686,6 +855,10 @@ def main() -> int:
         multi.set_scene(c5prims)
         rend.set_scene(c5prims)
         layouts = (1, 0) if multi.nranks > 1 else (0,)
+        # per-frame exchange for these 400-MB frames (the batched one would need 2 B frame
+        # buffers; a c5 part's exchange calls are negligible next to its 0.3 ms render)
+        if multi.nranks > 1:
+            multi.set_option(capi.RT_OPT_MULTI_BATCH, 1)
         c5 = {"workload": f"c5:{c5cfg.width}x{c5cfg.height}:d{c5cfg.depth}:s256w0",
               "precision": args.precision, "frames": c5n}
         # census of this rank's rows (interleaved parts: same total as any layout)
@@ -725,8 +898,17 @@ def main() -> int:
                         "mrays_per_s": round(c5segs * c5n / float(t5.item()) / 1e6, 1)}
         c5["segments_per_frame"] = c5segs
         multi.set_option(capi.RT_OPT_MULTI_LAYOUT, 0)
+        if multi.nranks > 1:
+            multi.set_option(capi.RT_OPT_MULTI_BATCH, rank_batch)
         del f5
 
+    # distinct GPUs under the ranks (a rehearsal runs several ranks on one GPU)
+    dv = torch.zeros(max(64, local + 1), dtype=torch.int64, device=dev)
+    dv[local] = 1
+    if world > 1:
+        dist.all_reduce(dv, op=dist.ReduceOp.MAX)
+    devices_used = int((dv > 0).sum().item())
+    PHASE[0] = "report"
     result = None
     if rank == 0:
         ms_step = elapsed_s / args.steps * 1e3
@@ -759,7 +941,7 @@ def main() -> int:
             "metric": METRIC,
             "value": round(value, 2),
             "unit": "Mrays/s",
-            "n_gpus": world,
+            "n_gpus": n_ranks,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 4),
@@ -789,6 +971,10 @@ def main() -> int:
                 "row_feedback": args.row_feedback,
                 "frames_in_flight": fif,
                 "backend": backend if world > 1 else None,
+                "transport": args.transport if world > 1 else None,
+                "devices": devices_used,
+                "rehearsal": devices_used < n_ranks,
+                "frame_buffers": nbuf,
             },
             "ms_per_frame": round(ms_step / frames_per_step, 4),
             "mpx_per_s": round(px_step * args.steps / elapsed_s / 1e6, 2),

@@ -222,9 +222,10 @@ enum rt_option {
                                          handle of one exchange must use the same F.  The
                                          gathered frames are identical. */
     RT_OPT_MULTI_FAULT = 18,         /* rt_multi_set_option only, a test hook: 1 = the next
-                                         frame of the process holding the root fails right
-                                         after its RCCL receives were queued (the failure
-                                         path of a real exchange on a one-GPU machine). */
+                                         frame (or batch) of this handle fails right after
+                                         its part of the exchange was queued — the root's
+                                         receives, a sender's send (the failure path of a
+                                         real exchange on a one-GPU machine). */
     RT_OPT_MULTI_BATCH = 19,         /* rt_multi_set_option only: B in [1,
                                          RT_MULTI_BATCH_MAX] (default 1) frames per gather in
                                          rt_multi_render_device_frames, one process per rank
@@ -241,9 +242,28 @@ enum rt_option {
                                          B > 1, nframes >= 2 and every camera has the same
                                          size (so every rank decides alike; every handle of
                                          one exchange must use the same B); the root then
-                                         takes at most RT_MULTI_SLOTS distinct caller streams
-                                         (else RT_ERR_UNSUPPORTED).  The frames are
+                                         needs a DISTINCT frame buffer for each frame of a
+                                         batch (min(B, nframes) of them: frames of one batch
+                                         sharing a buffer could never be whole in it) and at
+                                         most RT_MULTI_SLOTS distinct caller streams, else
+                                         the call is refused before anything is enqueued
+                                         (RT_ERR_UNSUPPORTED; with ranks in other processes
+                                         the exchange is then broken, as the peers' sends of
+                                         that call have no receives).  A buffer of an earlier
+                                         batch is rendered into again only after that
+                                         batch's gather into it completed, so every frame is
+                                         whole in its buffer from its batch's end until the
+                                         next frame written there (2 B buffers keep
+                                         consecutive batches overlapped).  The frames are
                                          identical. */
+    RT_OPT_MULTI_TIMEOUT_MS = 20,    /* rt_multi_set_option only: T >= 0 (default 120000)
+                                         ms that rt_multi_sync waits for this process's
+                                         streams; it polls them (and RCCL's asynchronous
+                                         error) and, when T passes or RCCL reports an error,
+                                         breaks the exchange, aborts the communicators
+                                         (ncclCommAbort) and returns RT_ERR_COMM instead of
+                                         blocking forever on a peer that failed.  0 = no
+                                         deadline. */
     RT_OPT_MULTI_LAYOUT = 13,        /* rt_multi_set_option only: 0 (default) = contiguous
                                          row bands (rt_band_rows); 1 = interleaved tile rows
                                          (rt_interleaved_rows): balanced when the frame's cost
@@ -328,15 +348,17 @@ int rt_render_device_frames(rt_ctx* ctx, const rt_camera* cams, int32_t ncams, i
  * are still being rendered or sent on its comm stream;
  * a band buffer is reused only after its send has completed (device-side event waits; the
  * host never blocks in rt_multi_render_device*).
- * Failures: a frame that fails on one rank after a local rank has queued its part of the
- * gather (a receive or a send) leaves the communicator out of step; the rt_multi is then
- * broken — every later frame returns RT_ERR_COMM, rt_multi_sync aborts the communicator
- * (ncclCommAbort) instead of waiting on receives that cannot complete, and
- * rt_multi_destroy aborts instead of destroying.  A frame that fails before any local
- * rank queued anything (no scene, an unsupported combination) returns its status and leaves
- * the rt_multi usable.  With one process per GPU this is local to the process that saw the
- * failure: the other processes are not told, and their sends, receives or rt_multi_sync can
- * block until their own communicator is aborted (RT_TRANSPORT_THREADS does tell its peers). */
+ * Failures: argument checks every rank makes alike return their status and leave the
+ * rt_multi usable.  A frame that fails after them leaves the exchange out of step when any
+ * rank may have queued its part (a receive or a send): always with ranks in other processes
+ * (they queue theirs whatever this process did), and with every rank in this process once
+ * a local rank queued its part.  The rt_multi is then broken — every later frame returns
+ * RT_ERR_COMM, rt_multi_sync aborts the communicator (ncclCommAbort) instead of waiting on
+ * receives that cannot complete, and rt_multi_destroy aborts instead of destroying.  With
+ * one process per GPU over RCCL the other processes are not told: their rt_multi_sync
+ * polls their streams and RCCL's asynchronous error and gives up at its deadline
+ * (RT_OPT_MULTI_TIMEOUT_MS: broken, communicator aborted, RT_ERR_COMM).  The mailbox
+ * transports (THREADS, IPC) tell every peer at once: their waits return RT_ERR_COMM. */
 #define RT_MULTI_ID_BYTES 128
 #define RT_MULTI_SLOTS 4   /* band slots per rank (RT_OPT_MULTI_FRAMES uses 1..4, default 2) */
 #define RT_MULTI_BATCH_MAX 16  /* frames per gather (RT_OPT_MULTI_BATCH) */
@@ -353,7 +375,19 @@ enum rt_transport {
      * on).  Handles may share a device.  The host calls of a frame block until the peer's
      * matching post (RCCL's never block); a handle's failure or destroy ends the exchange
      * for all of them (RT_ERR_COMM, no hang). */
-    RT_TRANSPORT_THREADS = 3
+    RT_TRANSPORT_THREADS = 3,
+    /* Rehearsal of the one-process-per-GPU model ACROSS processes, one per rank (nlocal = 1,
+     * first_rank = its rank, the same unique_id — any RT_MULTI_ID_BYTES bytes the processes
+     * share, e.g. random ones — naming a POSIX shared-memory mailbox; at most 64 ranks).
+     * The THREADS protocol between processes: the root's staging buffers and every rank's
+     * exchange events are shared once with hipIpcGetMemHandle / hipIpcGetEventHandle; a
+     * sender's comm stream waits on the root's "ready" event, copies its part into the
+     * root's staging buffer and records its "sent" event, on which the root's comm stream
+     * waits before copying the part into the frame rows.  Processes may share a device (one
+     * GPU).  rt_multi_create blocks until every rank has joined; the segment's name is
+     * removed once all have.  A rank's failure ends the exchange for all of them
+     * (RT_ERR_COMM); a peer process that exits is detected. */
+    RT_TRANSPORT_IPC = 4
 };
 typedef struct rt_multi rt_multi;
 

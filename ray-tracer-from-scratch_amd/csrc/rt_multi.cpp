@@ -33,13 +33,33 @@
  * which the root's comm stream waits.  So a one-GPU box runs every branch a process-per-GPU
  * RCCL run takes (the non-root enqueue, the caller-stream wait on the send, the root's
  * interleaved staging and scatter) except the RCCL calls themselves.
+ *
+ * RT_TRANSPORT_IPC (rehearsal across processes): the same mailbox protocol between real
+ * processes, one per rank, on one GPU or several.  The mailbox is a POSIX shared-memory
+ * segment named after the unique id (one ring of posts per direction and non-root rank);
+ * the root's staging buffers and every rank's exchange events are shared with
+ * hipIpcGetMemHandle / hipIpcGetEventHandle once, at create (staging buffers again when they
+ * grow).  A sender's comm stream waits on the root's imported "ready" event, copies its
+ * part into the root's staging buffer through the imported mapping and records its own
+ * "sent" event, which the root's comm stream waits on before copying the part into the
+ * frame rows.  So bench.py's process-per-GPU code (its non-root branches, the broadcasts of
+ * the id and the row weights) runs in separate processes on a one-GPU box.
  */
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <fcntl.h>
+#include <signal.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <array>
 #include <atomic>
+#include <cerrno>
 #include <chrono>
+#include <cmath>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstdio>
@@ -96,6 +116,9 @@ struct Rank {
     void* bstage[2] = {};
     size_t bstage_cap = 0;
     hipEvent_t ev_brend[2][RT_MULTI_SLOTS] = {}, ev_bsent[2] = {};
+    // root: batch slot b's scatter into its frames is complete (a later batch renders into
+    // one of those frame buffers only after it, so every frame is whole in its buffer)
+    hipEvent_t ev_bdone[2] = {};
     // worker thread (local ranks other than the first, one process driving several GPUs)
     std::thread th;
     std::mutex mu;
@@ -115,6 +138,7 @@ struct Post {
     size_t bytes = 0;
     hipEvent_t ev = nullptr;  // root -> sender: the destination may be written after it;
                               // sender -> root: the copy is complete after it
+    const void* owner = nullptr;  // the posting handle (its posts go when it is destroyed)
 };
 struct Hub {
     std::mutex mu;
@@ -125,6 +149,54 @@ struct Hub {
 };
 std::mutex g_hubs_mu;
 std::map<std::string, std::shared_ptr<Hub>> g_hubs;
+
+/* RT_TRANSPORT_IPC mailbox: one shared-memory segment per unique id, zero-filled by
+ * ftruncate and accessed with __atomic builtins only (plain fields, no constructors run in
+ * shared memory).  Each non-root rank g has two single-producer rings: `recv` (the root posts
+ * where g's part of a frame/batch lands) and `sent` (g posts that its copy was enqueued). */
+constexpr int IPC_MAX_RANKS = 64;
+constexpr int IPC_RING = 16;
+// the exchange events every rank exports: ev_ready[slot] (root), ev_sent[slot], ev_bsent[b]
+enum : int { EV_READY = 0, EV_SENT = RT_MULTI_SLOTS, EV_BSENT = 2 * RT_MULTI_SLOTS, IPC_NEV = EV_BSENT + 2 };
+struct IpcMsg {
+    uint64_t seq;       // n + 1 once message n of the ring is written (release)
+    uint64_t frame, bytes, offset;
+    uint32_t alloc;     // root -> sender: id of the root's exported staging allocation
+    int32_t ev;         // the poster's event (EV_*) to wait on
+    hipIpcMemHandle_t mem;  // root -> sender: that allocation's handle
+};
+struct IpcRing {
+    IpcMsg msg[IPC_RING];
+    uint64_t taken;     // messages consumed (release)
+};
+struct IpcPeer {
+    uint32_t joined, left;  // set once (release): handles written / imports closed
+    int32_t pid, nranks;
+    hipIpcEventHandle_t ev[IPC_NEV];
+    IpcRing recv, sent;
+};
+struct IpcShared {
+    uint32_t failed;        // a handle failed mid-exchange: every wait gives up
+    int32_t failed_rank;
+    IpcPeer peer[IPC_MAX_RANKS];
+};
+struct Ipc {
+    IpcShared* sh = nullptr;
+    std::string name;
+    bool unlinked = false, joined = false;
+    std::vector<std::array<hipEvent_t, IPC_NEV>> imp;  // the peers' events opened here
+    struct Exp {
+        void* base;
+        size_t bytes;
+        uint32_t id;
+        hipIpcMemHandle_t h;
+    };
+    std::vector<Exp> exp;                 // root: exported staging allocations (freed at destroy)
+    uint32_t next_id = 1;
+    std::map<uint32_t, void*> opened;     // sender: the root's allocations mapped here
+    std::vector<uint64_t> nrecv, nsent;   // root: posts made / taken per rank
+    uint64_t nrecv_taken = 0, nsent_posted = 0;  // sender
+};
 
 }  // namespace
 
@@ -153,13 +225,19 @@ struct rt_multi {
     std::atomic<bool> queued{false};
     std::shared_ptr<Hub> hub;       // RT_TRANSPORT_THREADS
     std::string hub_key;
+    std::unique_ptr<Ipc> ipc;       // RT_TRANSPORT_IPC
+    int64_t timeout_ms = 120000;    // RT_OPT_MULTI_TIMEOUT_MS (rt_multi_sync's deadline)
+    std::vector<char*> batch_bufs[2];  // root: the frame buffers of batch slot 0 / 1
     bool has_root() const { return first_rank == 0; }
     bool rccl() const { return transport == RT_TRANSPORT_RCCL || transport == RT_TRANSPORT_RCCL_LOOPBACK; }
     bool loopback() const { return transport == RT_TRANSPORT_RCCL_LOOPBACK; }
     bool threads() const { return transport == RT_TRANSPORT_THREADS; }
+    bool via_ipc() const { return transport == RT_TRANSPORT_IPC; }
+    // the mailbox transports: every ncclSend/ncclRecv pair is a copy matched through posts
+    bool mailbox() const { return threads() || via_ipc(); }
     // the frame goes through an exchange between ranks (a communicator with several ranks or
-    // the root's band to itself, or the THREADS mailbox); COPY writes the root's frame directly
-    bool gathers() const { return (rccl() && (nranks > 1 || loopback())) || threads(); }
+    // the root's band to itself, or a mailbox); COPY writes the root's frame directly
+    bool gathers() const { return (rccl() && (nranks > 1 || loopback())) || mailbox(); }
 };
 
 namespace {
@@ -253,6 +331,20 @@ void hub_fail(rt_multi* m) {
     }
     m->hub->cv.notify_all();
 }
+/* A handle going away: the exchange ends for its peers, and its posts (which name its
+ * events) are withdrawn under the lock — a taker enqueues its wait on a post's event while
+ * holding the lock (hub_take), so no wait can reach an event after this returns. */
+void hub_leave(rt_multi* m) {
+    if (!m->hub) return;
+    {
+        std::lock_guard<std::mutex> lk(m->hub->mu);
+        m->hub->failed = true;
+        for (auto* mp : {&m->hub->recv, &m->hub->sent})
+            for (auto it = mp->begin(); it != mp->end();)
+                it = it->second.owner == m ? mp->erase(it) : std::next(it);
+    }
+    m->hub->cv.notify_all();
+}
 void hub_put(rt_multi* m, std::map<std::pair<uint64_t, int>, Post> Hub::*box, uint64_t frame, int rank,
              const Post& p) {
     {
@@ -261,9 +353,10 @@ void hub_put(rt_multi* m, std::map<std::pair<uint64_t, int>, Post> Hub::*box, ui
     }
     m->hub->cv.notify_all();
 }
-/* Blocks until the peer has posted (frame, rank) into `box`, then takes the post. */
+/* Blocks until the peer has posted (frame, rank) into `box`, then takes the post and, if
+ * wait_on is set, makes that stream wait on the post's event (still under the lock). */
 int hub_take(rt_multi* m, std::map<std::pair<uint64_t, int>, Post> Hub::*box, uint64_t frame, int rank,
-             Post* out, const char* what) {
+             Post* out, const char* what, hipStream_t wait_on) {
     Hub& h = *m->hub;
     std::unique_lock<std::mutex> lk(h.mu);
     auto& mp = h.*box;
@@ -279,7 +372,227 @@ int hub_take(rt_multi* m, std::map<std::pair<uint64_t, int>, Post> Hub::*box, ui
     }
     *out = it->second;
     mp.erase(it);
+    if (wait_on && out->ev) MHIPF(m, hipStreamWaitEvent(wait_on, out->ev, 0));
     return RT_OK;
+}
+
+/* ---- RT_TRANSPORT_IPC mailbox (shared memory between processes) ---- */
+template <class T>
+T ld_acq(const T* p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
+template <class T>
+void st_rel(T* p, T v) { __atomic_store_n(p, v, __ATOMIC_RELEASE); }
+
+void ipc_fail(rt_multi* m) {
+    if (!m->ipc || !m->ipc->sh) return;
+    int32_t none = 0;
+    (void)__atomic_compare_exchange_n(&m->ipc->sh->failed_rank, &none, m->first_rank + 1, false,
+                                      __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE);
+    st_rel(&m->ipc->sh->failed, 1u);
+}
+bool pid_gone(int32_t pid) { return pid > 0 && ::kill(pid, 0) != 0 && errno == ESRCH; }
+/* Polls `ready` (yield first, then 20-us sleeps) until it holds, a handle failed, the peer's
+ * process is gone, or ms passes. */
+template <class Pred>
+int ipc_wait(rt_multi* m, Pred ready, int peer, const char* what, int64_t ms) {
+    IpcShared* sh = m->ipc->sh;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int it = 0;; it++) {
+        if (ready()) return RT_OK;
+        const char* why = nullptr;
+        if (ld_acq(&sh->failed)) why = "a peer handle failed";
+        if (!why && it >= 2048) {
+            if ((it & 255) == 0 && peer >= 0 && pid_gone(sh->peer[peer].pid)) why = "the peer's process exited";
+            else if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(ms)) why = "timed out";
+        }
+        if (why) {
+            const int32_t fr = ld_acq(&sh->failed_rank);
+            std::snprintf(m->last_err, sizeof m->last_err, "%s (peer rank %d): %s%s", what, peer, why,
+                          fr > 0 ? (std::string(" (rank ") + std::to_string(fr - 1) + " failed first)").c_str() : "");
+            return RT_ERR_COMM;
+        }
+        if (it < 2048) std::this_thread::yield();
+        else std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+}
+int ipc_post(rt_multi* m, IpcRing& r, uint64_t& count, const IpcMsg& v, int peer, const char* what) {
+    int st = ipc_wait(m, [&] { return count - ld_acq(&r.taken) < (uint64_t)IPC_RING; }, peer, what,
+                      hub_timeout_ms());
+    if (st != RT_OK) return st;
+    IpcMsg& e = r.msg[count % IPC_RING];
+    e.frame = v.frame;
+    e.bytes = v.bytes;
+    e.offset = v.offset;
+    e.alloc = v.alloc;
+    e.ev = v.ev;
+    e.mem = v.mem;
+    st_rel(&e.seq, count + 1);
+    count++;
+    return RT_OK;
+}
+int ipc_take(rt_multi* m, IpcRing& r, uint64_t& count, uint64_t frame, IpcMsg* out, int peer, const char* what) {
+    IpcMsg& e = r.msg[count % IPC_RING];
+    const uint64_t want = count + 1;
+    int st = ipc_wait(m, [&] { return ld_acq(&e.seq) == want; }, peer, what, hub_timeout_ms());
+    if (st != RT_OK) return st;
+    out->frame = e.frame;
+    out->bytes = e.bytes;
+    out->offset = e.offset;
+    out->alloc = e.alloc;
+    out->ev = e.ev;
+    out->mem = e.mem;
+    st_rel(&r.taken, want);
+    count++;
+    if (out->frame != frame || out->ev < 0 || out->ev >= IPC_NEV) {
+        std::snprintf(m->last_err, sizeof m->last_err, "%s (peer rank %d): post for frame %llu, expected %llu",
+                      what, peer, (unsigned long long)out->frame, (unsigned long long)frame);
+        return RT_ERR_COMM;
+    }
+    return RT_OK;
+}
+/* A staging buffer of the root that senders write into: hipMalloc'd and exported once; kept
+ * until destroy (a peer may still hold the mapping when it grows). */
+int ipc_alloc(rt_multi* m, size_t bytes, void** out) {
+    *out = nullptr;
+    Ipc::Exp e{};
+    MHIP(m, hipMalloc(&e.base, bytes));
+    e.bytes = bytes;
+    e.id = m->ipc->next_id++;
+    const hipError_t he = hipIpcGetMemHandle(&e.h, e.base);
+    if (he != hipSuccess) {
+        (void)hipFree(e.base);
+        return hip_err(m, he, "hipIpcGetMemHandle");
+    }
+    m->ipc->exp.push_back(e);
+    *out = e.base;
+    return RT_OK;
+}
+
+/* The exchange events of a rank by EV_* index. */
+hipEvent_t local_ev(Rank* k, int idx) {
+    if (idx < EV_SENT) return k->ev_ready[idx - EV_READY];
+    if (idx < EV_BSENT) return k->ev_sent[idx - EV_SENT];
+    return k->ev_bsent[idx - EV_BSENT];
+}
+
+/* ---- the mailbox transports' four operations (THREADS: the in-process Hub; IPC: rings) ---- */
+/* Root: rank g's part of `frame` (a frame or a batch's first frame) lands at dst (bytes)
+ * once the root's event ev_idx has fired. */
+int mbox_post_recv(rt_multi* m, Rank* k, uint64_t frame, int g, char* dst, size_t bytes, int ev_idx) {
+    if (m->threads()) {
+        Post p;
+        p.dst = dst;
+        p.device = k->device;
+        p.bytes = bytes;
+        p.ev = local_ev(k, ev_idx);
+        p.owner = m;
+        hub_put(m, &Hub::recv, frame, g, p);
+        return RT_OK;
+    }
+    Ipc& x = *m->ipc;
+    const Ipc::Exp* a = nullptr;
+    for (const auto& e : x.exp)
+        if (dst >= static_cast<char*>(e.base) && dst + bytes <= static_cast<char*>(e.base) + e.bytes) a = &e;
+    if (!a) {
+        std::snprintf(m->last_err, sizeof m->last_err, "IPC: rank %d's destination is not an exported buffer", g);
+        return RT_ERR_COMM;
+    }
+    IpcMsg v{};
+    v.frame = frame;
+    v.bytes = bytes;
+    v.offset = (uint64_t)(dst - static_cast<char*>(a->base));
+    v.alloc = a->id;
+    v.ev = ev_idx;
+    v.mem = a->h;
+    return ipc_post(m, x.sh->peer[g].recv, x.nrecv[g], v, g, "posting a receive");
+}
+/* Sender: where this rank's part of `frame` goes (*dst on device *dev); `st` waits until it
+ * may be written. */
+int mbox_take_recv(rt_multi* m, Rank* k, uint64_t frame, size_t bytes, hipStream_t st, char** dst, int* dev) {
+    if (m->threads()) {
+        Post p;
+        const int e = hub_take(m, &Hub::recv, frame, k->rank, &p, "waiting for the root's receive", st);
+        if (e != RT_OK) return e;
+        if (p.bytes != bytes) {
+            std::snprintf(m->last_err, sizeof m->last_err, "rank %d: the root expects %zu bytes, the part has %zu",
+                          k->rank, p.bytes, bytes);
+            return RT_ERR_COMM;
+        }
+        *dst = static_cast<char*>(p.dst);
+        *dev = p.device;
+        return RT_OK;
+    }
+    Ipc& x = *m->ipc;
+    IpcMsg v{};
+    int e = ipc_take(m, x.sh->peer[k->rank].recv, x.nrecv_taken, frame, &v, 0, "waiting for the root's receive");
+    if (e != RT_OK) return e;
+    if (v.bytes != bytes) {
+        std::snprintf(m->last_err, sizeof m->last_err, "rank %d: the root expects %llu bytes, the part has %zu",
+                      k->rank, (unsigned long long)v.bytes, bytes);
+        return RT_ERR_COMM;
+    }
+    auto it = x.opened.find(v.alloc);
+    if (it == x.opened.end()) {
+        void* p = nullptr;
+        MHIP(m, hipIpcOpenMemHandle(&p, v.mem, hipIpcMemLazyEnablePeerAccess));
+        it = x.opened.emplace(v.alloc, p).first;
+    }
+    *dst = static_cast<char*>(it->second) + v.offset;
+    *dev = k->device;
+    if (!x.imp[0][v.ev]) {
+        std::snprintf(m->last_err, sizeof m->last_err, "IPC: the root posted event %d, not imported", v.ev);
+        return RT_ERR_COMM;
+    }
+    MHIPF(m, hipStreamWaitEvent(st, x.imp[0][v.ev], 0));
+    return RT_OK;
+}
+/* Sender: this rank's copy of `frame`'s part is complete once its event ev_idx fires. */
+int mbox_post_sent(rt_multi* m, Rank* k, uint64_t frame, int ev_idx) {
+    if (m->threads()) {
+        Post p;
+        p.ev = local_ev(k, ev_idx);
+        p.owner = m;
+        hub_put(m, &Hub::sent, frame, k->rank, p);
+        return RT_OK;
+    }
+    Ipc& x = *m->ipc;
+    IpcMsg v{};
+    v.frame = frame;
+    v.ev = ev_idx;
+    return ipc_post(m, x.sh->peer[k->rank].sent, x.nsent_posted, v, 0, "posting a send");
+}
+/* Root: `st` waits until rank g's part of `frame` has landed. */
+int mbox_take_sent(rt_multi* m, Rank* k, uint64_t frame, int g, hipStream_t st) {
+    (void)k;
+    if (m->threads()) {
+        Post p;
+        return hub_take(m, &Hub::sent, frame, g, &p, "waiting for a part's copy", st);
+    }
+    Ipc& x = *m->ipc;
+    IpcMsg v{};
+    const int e = ipc_take(m, x.sh->peer[g].sent, x.nsent[g], frame, &v, g, "waiting for a part's copy");
+    if (e != RT_OK) return e;
+    if (!x.imp[g][v.ev]) {
+        std::snprintf(m->last_err, sizeof m->last_err, "IPC: rank %d posted event %d, not imported", g, v.ev);
+        return RT_ERR_COMM;
+    }
+    MHIPF(m, hipStreamWaitEvent(st, x.imp[g][v.ev], 0));
+    return RT_OK;
+}
+/* A sender's copy into the destination mbox_take_recv returned. */
+int mbox_copy(rt_multi* m, Rank* k, char* dst, int dev, const void* src, size_t bytes, hipStream_t st) {
+    if (m->threads()) MHIPF(m, hipMemcpyPeerAsync(dst, dev, src, k->device, bytes, st));
+    else MHIPF(m, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st));
+    return RT_OK;
+}
+
+/* RT_OPT_MULTI_FAULT (test hook): this frame fails here, once this rank's part of the
+ * exchange has been queued. */
+bool injected(rt_multi* m) {
+    if (!m->fault_next) return false;
+    m->fault_next = false;
+    std::snprintf(m->last_err, sizeof m->last_err,
+                  "injected fault (rank %d) after its part of the exchange was queued", m->first_rank);
+    return true;
 }
 
 /* Band buffers of a rank, grown (rarely) to `bytes` each: a non-root rank renders into them
@@ -394,45 +707,57 @@ int enqueue_rank(rt_multi* m, Rank* k, const Job& j) {
         if (m->gathers()) {
             m->queued.store(true, std::memory_order_relaxed);
             const size_t part_bytes = (size_t)max_part_rows(m, cam.height) * row_bytes;
-            if (inter && part_bytes * m->nranks > k->staging_cap) {
+            // parts land in staging (then go to their rows on the comm stream): interleaved
+            // parts always; every part under IPC (senders write only exported buffers)
+            const bool staged = inter || m->via_ipc();
+            if (staged && part_bytes * m->nranks > k->staging_cap) {
                 // grow (rare): the comm stream may still scatter from the old buffers
                 MHIP(m, hipStreamSynchronize(k->comm_stream));
                 for (auto& b : k->staging) {
-                    if (b) MHIP(m, hipFree(b));
+                    if (b && !m->via_ipc()) MHIP(m, hipFree(b));  // IPC: kept until destroy
                     b = nullptr;
                 }
                 k->staging_cap = 0;
-                for (auto& b : k->staging) MHIP(m, hipMalloc(&b, part_bytes * m->nranks));
+                for (auto& b : k->staging) {
+                    if (m->via_ipc()) {
+                        st = ipc_alloc(m, part_bytes * m->nranks, &b);
+                        if (st != RT_OK) return st;
+                    } else {
+                        MHIP(m, hipMalloc(&b, part_bytes * m->nranks));
+                    }
+                }
                 k->staging_cap = part_bytes * m->nranks;
             }
             MHIPF(m, hipStreamWaitEvent(k->comm_stream, j.ev_in, 0));
-            if (m->threads()) {
+            if (m->mailbox()) {
                 // the mailbox's receives: post where every part lands (after ev_ready: the
                 // caller's earlier work on the frame is done), then wait on each part's copy
                 MHIPF(m, hipEventRecord(k->ev_ready[s], k->comm_stream));
                 for (int g = 1; g < m->nranks; g++) {
                     const Part pg = part_of(m, cam.height, g);
                     if (pg.nrows <= 0 || row_bytes == 0) continue;
-                    Post p;
-                    p.dst = inter ? static_cast<char*>(k->staging[s]) + (size_t)g * part_bytes
-                                  : j.d_frame + (size_t)pg.row0 * row_bytes;
-                    p.device = k->device;
-                    p.bytes = (size_t)pg.nrows * row_bytes;
-                    p.ev = k->ev_ready[s];
-                    hub_put(m, &Hub::recv, m->frame, g, p);
+                    char* dst = staged ? static_cast<char*>(k->staging[s]) + (size_t)g * part_bytes
+                                       : j.d_frame + (size_t)pg.row0 * row_bytes;
+                    st = mbox_post_recv(m, k, m->frame, g, dst, (size_t)pg.nrows * row_bytes, EV_READY + s);
+                    if (st != RT_OK) return st;
                 }
+                if (injected(m)) return RT_ERR_HIP;
                 for (int g = 1; g < m->nranks; g++) {
                     const Part pg = part_of(m, cam.height, g);
                     if (pg.nrows <= 0 || row_bytes == 0) continue;
-                    Post p;
-                    st = hub_take(m, &Hub::sent, m->frame, g, &p, "waiting for a part's copy");
+                    st = mbox_take_sent(m, k, m->frame, g, k->comm_stream);
                     if (st != RT_OK) return st;
-                    MHIPF(m, hipStreamWaitEvent(k->comm_stream, p.ev, 0));
                 }
-                if (inter)
+                if (staged)
                     for (int g = 1; g < m->nranks; g++) {
-                        st = scatter_part(m, j.d_frame, static_cast<char*>(k->staging[s]) + (size_t)g * part_bytes,
-                                          cam.height, g, row_bytes, k->comm_stream);
+                        const Part pg = part_of(m, cam.height, g);
+                        const char* src = static_cast<char*>(k->staging[s]) + (size_t)g * part_bytes;
+                        if (inter)
+                            st = scatter_part(m, j.d_frame, src, cam.height, g, row_bytes, k->comm_stream);
+                        else if (pg.nrows > 0 && row_bytes > 0)
+                            MHIPF(m, hipMemcpyAsync(j.d_frame + (size_t)pg.row0 * row_bytes, src,
+                                                    (size_t)pg.nrows * row_bytes, hipMemcpyDeviceToDevice,
+                                                    k->comm_stream));
                         if (st != RT_OK) return st;
                     }
                 MHIPF(m, hipEventRecord(k->ev_done, k->comm_stream));
@@ -463,11 +788,7 @@ int enqueue_rank(rt_multi* m, Rank* k, const Job& j) {
                 }
             }
             MNCCL(m, ncclGroupEnd());
-            if (m->fault_next) {  // RT_OPT_MULTI_FAULT (tests): fail once the gather is queued
-                m->fault_next = false;
-                std::snprintf(m->last_err, sizeof m->last_err, "injected fault after the gather was queued");
-                return RT_ERR_HIP;
-            }
+            if (injected(m)) return RT_ERR_HIP;
             if (inter)
                 for (int g = lb ? 0 : 1; g < m->nranks; g++) {
                     st = scatter_part(m, j.d_frame, static_cast<char*>(k->staging[s]) + (size_t)g * part_bytes,
@@ -495,22 +816,19 @@ int enqueue_rank(rt_multi* m, Rank* k, const Job& j) {
     m->queued.store(true, std::memory_order_relaxed);
     if (m->rccl()) {
         MNCCL(m, ncclSend(k->band[s], bytes, ncclUint8, 0, k->comm, k->comm_stream));
-    } else if (m->threads()) {
+        if (injected(m)) return RT_ERR_HIP;
+    } else if (m->mailbox()) {
         // the mailbox's send: where the root wants this part, once it may be written
-        Post p;
-        st = hub_take(m, &Hub::recv, m->frame, k->rank, &p, "waiting for the root's receive");
+        char* dst = nullptr;
+        int ddev = 0;
+        st = mbox_take_recv(m, k, m->frame, bytes, k->comm_stream, &dst, &ddev);
         if (st != RT_OK) return st;
-        if (p.bytes != bytes) {
-            std::snprintf(m->last_err, sizeof m->last_err, "rank %d: the root expects %zu bytes, the part has %zu",
-                          k->rank, p.bytes, bytes);
-            return RT_ERR_COMM;
-        }
-        MHIPF(m, hipStreamWaitEvent(k->comm_stream, p.ev, 0));
-        MHIPF(m, hipMemcpyPeerAsync(p.dst, p.device, k->band[s], k->device, bytes, k->comm_stream));
+        st = mbox_copy(m, k, dst, ddev, k->band[s], bytes, k->comm_stream);
+        if (st != RT_OK) return st;
         MHIPF(m, hipEventRecord(k->ev_sent[s], k->comm_stream));
-        Post done;
-        done.ev = k->ev_sent[s];
-        hub_put(m, &Hub::sent, m->frame, k->rank, done);
+        st = mbox_post_sent(m, k, m->frame, EV_SENT + s);
+        if (st != RT_OK) return st;
+        if (injected(m)) return RT_ERR_HIP;
     } else {
         // the root's rows may still be read by the caller's earlier work on the frame buffer
         MHIPF(m, hipStreamWaitEvent(k->comm_stream, j.ev_in, 0));
@@ -523,7 +841,7 @@ int enqueue_rank(rt_multi* m, Rank* k, const Job& j) {
                                        k->device, bytes, k->comm_stream));
         }
     }
-    if (!m->threads()) MHIPF(m, hipEventRecord(k->ev_sent[s], k->comm_stream));  // THREADS: above
+    if (!m->mailbox()) MHIPF(m, hipEventRecord(k->ev_sent[s], k->comm_stream));  // mailbox: above
     // a process without the root: work the caller enqueues later on its stream (on this
     // rank's device) follows the band's send
     if (j.stream && !m->has_root())
@@ -652,33 +970,49 @@ int batch_send(rt_multi* m, Rank* k, const BatchJob& b, bool self) {
     if (m->rccl()) {
         MNCCL(m, ncclSend(k->bbuf[b.bs], total, ncclUint8, 0, k->comm, k->comm_stream));
         MHIPF(m, hipEventRecord(k->ev_bsent[b.bs], k->comm_stream));
-        return RT_OK;
+        return injected(m) ? RT_ERR_HIP : RT_OK;
     }
-    // THREADS: the mailbox's send, keyed by the batch's first frame
-    Post p;
-    int st = hub_take(m, &Hub::recv, m->frame, k->rank, &p, "waiting for the root's batch receive");
+    // the mailbox's send, keyed by the batch's first frame
+    char* dst = nullptr;
+    int ddev = 0;
+    int st = mbox_take_recv(m, k, m->frame, total, k->comm_stream, &dst, &ddev);
     if (st != RT_OK) return st;
-    if (p.bytes != total) {
-        std::snprintf(m->last_err, sizeof m->last_err, "rank %d: the root expects %zu bytes, the batch has %zu",
-                      k->rank, p.bytes, total);
-        return RT_ERR_COMM;
-    }
-    MHIPF(m, hipStreamWaitEvent(k->comm_stream, p.ev, 0));
-    MHIPF(m, hipMemcpyPeerAsync(p.dst, p.device, k->bbuf[b.bs], k->device, total, k->comm_stream));
+    st = mbox_copy(m, k, dst, ddev, k->bbuf[b.bs], total, k->comm_stream);
+    if (st != RT_OK) return st;
     MHIPF(m, hipEventRecord(k->ev_bsent[b.bs], k->comm_stream));
-    Post done;
-    done.ev = k->ev_bsent[b.bs];
-    hub_put(m, &Hub::sent, m->frame, k->rank, done);
-    return RT_OK;
+    st = mbox_post_sent(m, k, m->frame, EV_BSENT + b.bs);
+    if (st != RT_OK) return st;
+    return injected(m) ? RT_ERR_HIP : RT_OK;
 }
 /* The root's batch: frames[i] / sts[i] = frame i's buffer and caller stream (distinct streams
- * listed in uniq, at most RT_MULTI_SLOTS). */
+ * listed in uniq, at most RT_MULTI_SLOTS; the kb buffers distinct, checked by the caller). */
 int batch_root(rt_multi* m, Rank* k, const BatchJob& b, char* const* frames, hipStream_t const* sts,
                const std::vector<hipStream_t>& uniq) {
     const rt_camera& cam = b.cams[0];
     const size_t row_bytes = (size_t)cam.width * bpp(b.out_format);
     const int N = m->nranks;
     const bool lb = m->loopback();
+    // a frame buffer of an earlier batch is rendered into again only once that batch's
+    // scatter has completed, so each frame is whole in its buffer between its batch's end and
+    // the next render into that buffer.  The previous batch's buffers wait on its done event;
+    // the one before's on ev_bdone[bs], which still holds that batch's record (and the comm
+    // stream runs batches in order, so it also covers every older one).
+    {
+        std::vector<std::pair<hipStream_t, int>> waits;
+        const int prev = 1 - b.bs;
+        for (int i = 0; i < b.kb; i++) {
+            int slot = -1;
+            if (std::find(m->batch_bufs[prev].begin(), m->batch_bufs[prev].end(), frames[i]) !=
+                m->batch_bufs[prev].end())
+                slot = prev;
+            else if (std::find(m->batch_bufs[b.bs].begin(), m->batch_bufs[b.bs].end(), frames[i]) !=
+                     m->batch_bufs[b.bs].end())
+                slot = b.bs;
+            if (slot >= 0 && std::find(waits.begin(), waits.end(), std::make_pair(sts[i], slot)) == waits.end())
+                waits.emplace_back(sts[i], slot);
+        }
+        for (const auto& w : waits) MHIPF(m, hipStreamWaitEvent(w.first, k->ev_bdone[w.second], 0));
+    }
     // the scatter overwrites rows of frames that the caller's earlier work may still read
     for (size_t u = 0; u < uniq.size(); u++) {
         MHIPF(m, hipEventRecord(m->ev_in[u], uniq[u]));
@@ -701,6 +1035,7 @@ int batch_root(rt_multi* m, Rank* k, const BatchJob& b, char* const* frames, hip
         st = ctx_err(m, k, e, "rt_render_device_frames (root batch)");
     }
     if (st != RT_OK) return st;
+    m->batch_bufs[b.bs].assign(frames, frames + b.kb);
     // every sender's kb parts back to back in bstage[bs]
     std::vector<size_t> off((size_t)N, 0), pb((size_t)N, 0);
     std::vector<Part> parts((size_t)N);
@@ -713,37 +1048,40 @@ int batch_root(rt_multi* m, Rank* k, const BatchJob& b, char* const* frames, hip
     }
     if (total == 0) {
         MHIPF(m, hipEventRecord(k->ev_done, k->comm_stream));
+        MHIPF(m, hipEventRecord(k->ev_bdone[b.bs], k->comm_stream));
         return RT_OK;
     }
     if (total > k->bstage_cap) {  // grow (rare): the comm stream may still scatter from them
         MHIP(m, hipStreamSynchronize(k->comm_stream));
         for (auto& p : k->bstage) {
-            if (p) MHIP(m, hipFree(p));
+            if (p && !m->via_ipc()) MHIP(m, hipFree(p));  // IPC: kept until destroy
             p = nullptr;
         }
         k->bstage_cap = 0;
-        for (auto& p : k->bstage) MHIP(m, hipMalloc(&p, total));
+        for (auto& p : k->bstage) {
+            if (m->via_ipc()) {
+                st = ipc_alloc(m, total, &p);
+                if (st != RT_OK) return st;
+            } else {
+                MHIP(m, hipMalloc(&p, total));
+            }
+        }
         k->bstage_cap = total;
     }
     char* stage = static_cast<char*>(k->bstage[b.bs]);
     m->queued.store(true, std::memory_order_relaxed);
-    if (m->threads()) {
+    if (m->mailbox()) {
         MHIPF(m, hipEventRecord(k->ev_ready[b.bs], k->comm_stream));
         for (int g = 1; g < N; g++) {
             if (pb[g] == 0) continue;
-            Post p;
-            p.dst = stage + off[g];
-            p.device = k->device;
-            p.bytes = (size_t)b.kb * pb[g];
-            p.ev = k->ev_ready[b.bs];
-            hub_put(m, &Hub::recv, m->frame, g, p);
+            st = mbox_post_recv(m, k, m->frame, g, stage + off[g], (size_t)b.kb * pb[g], EV_READY + b.bs);
+            if (st != RT_OK) return st;
         }
+        if (injected(m)) return RT_ERR_HIP;
         for (int g = 1; g < N; g++) {
             if (pb[g] == 0) continue;
-            Post p;
-            st = hub_take(m, &Hub::sent, m->frame, g, &p, "waiting for a batch's copy");
+            st = mbox_take_sent(m, k, m->frame, g, k->comm_stream);
             if (st != RT_OK) return st;
-            MHIPF(m, hipStreamWaitEvent(k->comm_stream, p.ev, 0));
         }
     } else {
         MNCCL(m, ncclGroupStart());
@@ -759,11 +1097,7 @@ int batch_root(rt_multi* m, Rank* k, const BatchJob& b, char* const* frames, hip
             }
         }
         MNCCL(m, ncclGroupEnd());
-        if (m->fault_next) {  // RT_OPT_MULTI_FAULT (tests): fail once the gather is queued
-            m->fault_next = false;
-            std::snprintf(m->last_err, sizeof m->last_err, "injected fault after the gather was queued");
-            return RT_ERR_HIP;
-        }
+        if (injected(m)) return RT_ERR_HIP;
     }
     std::vector<ScatterSeg> segs;
     std::vector<int> fidx;
@@ -777,6 +1111,7 @@ int batch_root(rt_multi* m, Rank* k, const BatchJob& b, char* const* frames, hip
     st = scatter_segments(m, segs, fidx, frames, k->comm_stream);
     if (st != RT_OK) return st;
     MHIPF(m, hipEventRecord(k->ev_done, k->comm_stream));
+    MHIPF(m, hipEventRecord(k->ev_bdone[b.bs], k->comm_stream));
     if (lb) MHIPF(m, hipEventRecord(k->ev_bsent[b.bs], k->comm_stream));  // bbuf slot free again
     return RT_OK;
 }
@@ -827,6 +1162,7 @@ void destroy_rank(Rank* k, bool abort_comm) {
         for (auto e : k->ev_brend[b])
             if (e) (void)hipEventDestroy(e);
         if (k->ev_bsent[b]) (void)hipEventDestroy(k->ev_bsent[b]);
+        if (k->ev_bdone[b]) (void)hipEventDestroy(k->ev_bdone[b]);
         if (k->bbuf[b]) (void)hipFree(k->bbuf[b]);
         if (k->bstage[b]) (void)hipFree(k->bstage[b]);
     }
@@ -841,6 +1177,10 @@ void destroy_rank(Rank* k, bool abort_comm) {
     delete k;
 }
 
+/* A tile-row weight both weight entry points accept: finite and >= 0 (NaN, negatives and inf
+ * rejected, so prefix sums and band cuts stay finite). */
+bool valid_weight(float w) { return w >= 0.0f && w <= 3.0e38f; }
+
 int check_args(const rt_multi* m, const rt_camera* cam, int32_t depth, int32_t precision,
                int32_t out_format) {
     if (!m || !cam) return RT_ERR_INVALID_ARG;
@@ -851,17 +1191,128 @@ int check_args(const rt_multi* m, const rt_camera* cam, int32_t depth, int32_t p
     return RT_OK;
 }
 
-/* A frame (or batch) failed: out of step only if some rank already queued its part of the
- * exchange (a failure before that — no scene, an unsupported combination — leaves the
- * communicator usable); THREADS handles count frames in step, so any failure ends the
- * exchange and wakes the peers' mailbox waits. */
+/* A frame (or batch) failed after its arguments were checked (checks every rank makes alike
+ * come first and leave the rt_multi usable).  With ranks in other processes (nlocal <
+ * nranks) the peers queue their parts of the exchange whatever this process did — a
+ * failure only here (a HIP error on this rank's band, its scene missing) leaves them out of
+ * step — so the exchange is broken; the mailbox transports also end it for their peers
+ * (their waits give up).  With every rank in this process, only a failure after a local rank
+ * queued its part breaks it. */
 void mark_failed(rt_multi* m) {
-    if (m->threads()) {
+    if (m->mailbox()) {
         m->broken = true;
         hub_fail(m);
-    } else if (m->gathers() && m->queued.load(std::memory_order_relaxed)) {
+        ipc_fail(m);
+    } else if (m->gathers() && (m->nlocal < m->nranks || m->queued.load(std::memory_order_relaxed))) {
         m->broken = true;
     }
+}
+
+/* ---- RT_TRANSPORT_IPC setup and teardown ---- */
+/* Opens (or creates) the id's segment, exports this rank's exchange events, waits until every
+ * rank has joined and imports the peers' events it waits on (root: every sender's sent
+ * events; a sender: the root's ready events). */
+int ipc_create(rt_multi* m, const uint8_t* id) {
+    m->ipc.reset(new (std::nothrow) Ipc());
+    if (!m->ipc) return RT_ERR_OUT_OF_MEMORY;
+    Ipc& x = *m->ipc;
+    char name[64];
+    int n = std::snprintf(name, sizeof name, "/rtamd-ipc-");
+    for (int i = 0; i < 16; i++) n += std::snprintf(name + n, sizeof name - n, "%02x", id[i]);
+    x.name = name;
+    const int fd = ::shm_open(name, O_CREAT | O_RDWR, 0600);
+    if (fd < 0) {
+        std::snprintf(m->last_err, sizeof m->last_err, "shm_open %s: %s", name, std::strerror(errno));
+        return RT_ERR_COMM;
+    }
+    void* p = MAP_FAILED;
+    if (::ftruncate(fd, (off_t)sizeof(IpcShared)) == 0)
+        p = ::mmap(nullptr, sizeof(IpcShared), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    const int err = errno;
+    ::close(fd);
+    if (p == MAP_FAILED) {
+        std::snprintf(m->last_err, sizeof m->last_err, "mapping %s: %s", name, std::strerror(err));
+        return RT_ERR_COMM;
+    }
+    x.sh = static_cast<IpcShared*>(p);
+    x.imp.assign((size_t)m->nranks, std::array<hipEvent_t, IPC_NEV>{});
+    x.nrecv.assign((size_t)m->nranks, 0);
+    x.nsent.assign((size_t)m->nranks, 0);
+    Rank* k = m->r[0];
+    DevGuard dg(k->device);
+    MHIP(m, dg.err);
+    IpcPeer& me = x.sh->peer[k->rank];
+    if (ld_acq(&me.joined)) {
+        std::snprintf(m->last_err, sizeof m->last_err, "IPC: rank %d joined %s twice", k->rank, name);
+        return RT_ERR_INVALID_ARG;
+    }
+    for (int i = 0; i < IPC_NEV; i++) MHIP(m, hipIpcGetEventHandle(&me.ev[i], local_ev(k, i)));
+    me.pid = (int32_t)::getpid();
+    me.nranks = m->nranks;
+    st_rel(&me.joined, 1u);
+    x.joined = true;
+    int st = ipc_wait(m, [&] {
+        for (int g = 0; g < m->nranks; g++)
+            if (!ld_acq(&x.sh->peer[g].joined)) return false;
+        return true;
+    }, -1, "IPC: waiting for every rank to join", std::max<int64_t>(hub_timeout_ms(), 120000));
+    if (st != RT_OK) return st;
+    for (int g = 0; g < m->nranks; g++)
+        if (x.sh->peer[g].nranks != m->nranks) {
+            std::snprintf(m->last_err, sizeof m->last_err, "IPC: rank %d has %d ranks, this rank %d", g,
+                          x.sh->peer[g].nranks, m->nranks);
+            return RT_ERR_INVALID_ARG;
+        }
+    if (m->has_root()) {
+        for (int g = 1; g < m->nranks; g++)
+            for (int i = EV_SENT; i < IPC_NEV; i++)
+                MHIP(m, hipIpcOpenEventHandle(&x.imp[g][i], x.sh->peer[g].ev[i]));
+        // every rank has the segment mapped: drop its name (nothing left in /dev/shm)
+        ::shm_unlink(name);
+        x.unlinked = true;
+    } else {
+        for (int i = EV_READY; i < EV_SENT; i++) MHIP(m, hipIpcOpenEventHandle(&x.imp[0][i], x.sh->peer[0].ev[i]));
+    }
+    return RT_OK;
+}
+/* Before this rank's exported events and buffers are destroyed: close what it imported, mark
+ * it left, and wait (bounded) until every peer has done the same, so no peer still uses them. */
+void ipc_leave(rt_multi* m) {
+    if (!m->ipc) return;
+    Ipc& x = *m->ipc;
+    if (x.sh) {
+        DevGuard dg(m->r.empty() ? 0 : m->r[0]->device);
+        for (auto& a : x.imp)
+            for (auto& e : a)
+                if (e) {
+                    (void)hipEventDestroy(e);
+                    e = nullptr;
+                }
+        for (auto& o : x.opened) (void)hipIpcCloseMemHandle(o.second);
+        x.opened.clear();
+        if (x.joined && !m->r.empty()) {
+            st_rel(&x.sh->peer[m->r[0]->rank].left, 1u);
+            const auto t0 = std::chrono::steady_clock::now();
+            for (int g = 0; g < m->nranks; g++) {
+                IpcPeer& pg = x.sh->peer[g];
+                while (ld_acq(&pg.joined) && !ld_acq(&pg.left) && !pid_gone(pg.pid) &&
+                       std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(hub_timeout_ms()))
+                    std::this_thread::sleep_for(std::chrono::microseconds(200));
+            }
+        }
+        ::munmap(x.sh, sizeof(IpcShared));
+        x.sh = nullptr;
+    }
+    if (!x.unlinked && !x.name.empty() && m->has_root()) ::shm_unlink(x.name.c_str());
+    x.unlinked = true;
+    // the root's exported staging buffers (the rank's pointers to them are dropped)
+    if (!m->r.empty()) {
+        Rank* k = m->r[0];
+        for (auto& b : k->staging) b = nullptr;
+        for (auto& b : k->bstage) b = nullptr;
+    }
+    for (auto& e : x.exp) (void)hipFree(e.base);
+    x.exp.clear();
 }
 
 /* rt_multi_render_device_frames in batches of m->batch frames (RT_OPT_MULTI_BATCH; the
@@ -1015,18 +1466,21 @@ int rt_multi_create(const int32_t* devices, int32_t nlocal, int32_t nranks, int3
     if (!devices || nlocal <= 0 || nranks <= 0 || first_rank < 0 || first_rank + nlocal > nranks)
         return RT_ERR_INVALID_ARG;
     if (transport != RT_TRANSPORT_RCCL && transport != RT_TRANSPORT_COPY &&
-        transport != RT_TRANSPORT_RCCL_LOOPBACK && transport != RT_TRANSPORT_THREADS)
+        transport != RT_TRANSPORT_RCCL_LOOPBACK && transport != RT_TRANSPORT_THREADS &&
+        transport != RT_TRANSPORT_IPC)
         return RT_ERR_INVALID_ARG;
     const bool one_process = nlocal == nranks;
     if (!one_process && (!unique_id || transport == RT_TRANSPORT_COPY))
         return transport == RT_TRANSPORT_COPY ? RT_ERR_UNSUPPORTED : RT_ERR_INVALID_ARG;
-    // THREADS: one handle per rank (the process-per-GPU shape), two ranks at least
-    if (transport == RT_TRANSPORT_THREADS && (nlocal != 1 || nranks < 2)) return RT_ERR_INVALID_ARG;
+    // THREADS / IPC: one handle per rank (the process-per-GPU shape), two ranks at least
+    if ((transport == RT_TRANSPORT_THREADS || transport == RT_TRANSPORT_IPC) && (nlocal != 1 || nranks < 2))
+        return RT_ERR_INVALID_ARG;
+    if (transport == RT_TRANSPORT_IPC && (!unique_id || nranks > IPC_MAX_RANKS)) return RT_ERR_INVALID_ARG;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return RT_ERR_NO_DEVICE;
     for (int L = 0; L < nlocal; L++)
         if (devices[L] < 0 || devices[L] >= ndev) return RT_ERR_NO_DEVICE;
-    if (transport != RT_TRANSPORT_COPY && transport != RT_TRANSPORT_THREADS)
+    if (transport != RT_TRANSPORT_COPY && transport != RT_TRANSPORT_THREADS && transport != RT_TRANSPORT_IPC)
         for (int a = 0; a < nlocal; a++)
             for (int b = a + 1; b < nlocal; b++)
                 if (devices[a] == devices[b]) return RT_ERR_UNSUPPORTED;  // RCCL: one rank per GPU
@@ -1058,22 +1512,25 @@ int rt_multi_create(const int32_t* devices, int32_t nlocal, int32_t nranks, int3
         }
         DevGuard dg(k->device);
         hipError_t e = dg.err;
+        // the events a peer process waits on (IPC): shareable with hipIpcGetEventHandle
+        const unsigned xf = hipEventDisableTiming | (transport == RT_TRANSPORT_IPC ? hipEventInterprocess : 0u);
         for (auto& rs : k->render_stream)
             if (e == hipSuccess) e = hipStreamCreateWithFlags(&rs, hipStreamNonBlocking);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&k->comm_stream, hipStreamNonBlocking);
         for (int s = 0; s < RT_MULTI_SLOTS && e == hipSuccess; s++) {
             e = hipEventCreateWithFlags(&k->ev_rendered[s], hipEventDisableTiming);
-            if (e == hipSuccess) e = hipEventCreateWithFlags(&k->ev_sent[s], hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&k->ev_sent[s], xf);
             // recorded once, so the first wait on a slot (no send yet) is already satisfied
             if (e == hipSuccess) e = hipEventRecord(k->ev_sent[s], k->comm_stream);
-            if (e == hipSuccess) e = hipEventCreateWithFlags(&k->ev_ready[s], hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&k->ev_ready[s], xf);
         }
         if (e == hipSuccess) e = hipEventCreateWithFlags(&k->ev_done, hipEventDisableTiming);
         for (int b = 0; b < 2 && e == hipSuccess; b++) {
             for (int j = 0; j < RT_MULTI_SLOTS && e == hipSuccess; j++)
                 e = hipEventCreateWithFlags(&k->ev_brend[b][j], hipEventDisableTiming);
-            if (e == hipSuccess) e = hipEventCreateWithFlags(&k->ev_bsent[b], hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&k->ev_bsent[b], xf);
             if (e == hipSuccess) e = hipEventRecord(k->ev_bsent[b], k->comm_stream);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&k->ev_bdone[b], hipEventDisableTiming);
         }
         if (e != hipSuccess) fail(hip_err(m, e, "rank streams/events"));
     }
@@ -1111,6 +1568,12 @@ int rt_multi_create(const int32_t* devices, int32_t nlocal, int32_t nranks, int3
         m->hub = h;
         std::lock_guard<std::mutex> lk2(h->mu);
         h->refs++;
+    }
+    if (st == RT_OK && transport == RT_TRANSPORT_IPC) {
+        // the events recorded above must be in the runtime before a peer opens them
+        DevGuard dg(m->r[0]->device);
+        if (hipStreamSynchronize(m->r[0]->comm_stream) != hipSuccess) fail(RT_ERR_HIP);
+        else fail(ipc_create(m, unique_id));
     }
     // one rank: the band is the frame and nothing is exchanged, so no communicator (RCCL's
     // init would only print its banner on stdout and start its proxy thread) — except for
@@ -1168,14 +1631,83 @@ void abort_comms(rt_multi* m) {
         }
 }
 
+/* Waits for every local rank's streams by polling (a blocking wait could never end when a
+ * peer process died with its part of the exchange outstanding): RCCL's asynchronous error is
+ * checked while waiting, and when it reports one or timeout_ms (> 0) passes, the exchange is
+ * broken, the communicators are aborted and RT_ERR_COMM is returned. */
+static int drain_streams(rt_multi* m, int64_t timeout_ms) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (Rank* k : m->r) {
+        DevGuard dg(k->device);
+        MHIP(m, dg.err);
+        hipStream_t ss[RT_MULTI_SLOTS + 1];
+        for (int s = 0; s < RT_MULTI_SLOTS; s++) ss[s] = k->render_stream[s];
+        ss[RT_MULTI_SLOTS] = k->comm_stream;
+        for (hipStream_t s : ss) {
+            if (!s) continue;
+            for (int it = 0;; it++) {
+                const hipError_t e = hipStreamQuery(s);
+                if (e == hipSuccess) break;
+                if (e != hipErrorNotReady) return hip_err(m, e, "hipStreamQuery");
+                const char* why = nullptr;
+                ncclResult_t async = ncclSuccess;
+                if (k->comm && (it & 63) == 0 && (ncclCommGetAsyncError(k->comm, &async) != ncclSuccess ||
+                                                  async != ncclSuccess))
+                    why = async != ncclSuccess ? ncclGetErrorString(async) : "ncclCommGetAsyncError failed";
+                else if (timeout_ms > 0 && (it & 15) == 0 &&
+                         std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeout_ms))
+                    why = "deadline passed (RT_OPT_MULTI_TIMEOUT_MS)";
+                if (why) {
+                    std::snprintf(m->last_err, sizeof m->last_err,
+                                  "rt_multi_sync (rank %d): %s with its exchange outstanding: communicator aborted",
+                                  k->rank, why);
+                    if (!m->broken) {
+                        m->broken = true;
+                        hub_fail(m);
+                        ipc_fail(m);
+                    }
+                    abort_comms(m);
+                    return RT_ERR_COMM;
+                }
+                if (it < 1024) std::this_thread::yield();
+                else std::this_thread::sleep_for(std::chrono::microseconds(50));
+            }
+        }
+        if (k->comm) {
+            ncclResult_t async = ncclSuccess;
+            MNCCL(m, ncclCommGetAsyncError(k->comm, &async));
+            if (async != ncclSuccess) {
+                m->broken = true;
+                abort_comms(m);
+                return nccl_err(m, async, "ncclCommGetAsyncError");
+            }
+        }
+    }
+    return RT_OK;
+}
+
 int rt_multi_destroy(rt_multi* m) {
     if (!m) return RT_ERR_INVALID_ARG;
     if (m->broken) abort_comms(m);
+    // THREADS: peers still waiting on this handle give up, and its posts (naming its events)
+    // are withdrawn before the events are destroyed
+    if (m->hub) hub_leave(m);
+    if (m->ipc) {
+        // IPC: this rank's streams drained, its imports closed, and the peers' likewise
+        // before its exported events and staging buffers go (ipc_leave waits for them)
+        for (Rank* k : m->r) {
+            DevGuard dg(k->device);
+            for (auto rs : k->render_stream)
+                if (rs) (void)hipStreamSynchronize(rs);
+            if (k->comm_stream) (void)hipStreamSynchronize(k->comm_stream);
+        }
+        ipc_leave(m);
+    }
     for (Rank* k : m->r) destroy_rank(k, m->broken);
     m->r.clear();
+    m->ipc.reset();
     if (m->hub) {
-        // peers still waiting on this handle give up; the last handle drops the mailbox
-        hub_fail(m);
+        // the last handle drops the mailbox
         std::lock_guard<std::mutex> lk(g_hubs_mu);
         bool last;
         {
@@ -1219,6 +1751,11 @@ int rt_multi_set_option(rt_multi* m, int32_t option, int64_t value) {
         m->slots = (int)value;
         return RT_OK;
     }
+    if (option == RT_OPT_MULTI_TIMEOUT_MS) {
+        if (value < 0) return RT_ERR_INVALID_ARG;
+        m->timeout_ms = value;
+        return RT_OK;
+    }
     if (option == RT_OPT_MULTI_BATCH) {
         if (value < 1 || value > RT_MULTI_BATCH_MAX) return RT_ERR_INVALID_ARG;
         m->batch = (int)value;  // takes effect from the next rt_multi_render_device_frames
@@ -1241,7 +1778,7 @@ int rt_multi_set_option(rt_multi* m, int32_t option, int64_t value) {
 int rt_multi_set_row_weights(rt_multi* m, const float* weights, int32_t n) {
     if (!m || n < 0 || (n > 0 && !weights)) return RT_ERR_INVALID_ARG;
     for (int32_t t = 0; t < n; t++)
-        if (!(weights[t] >= 0.0f) || weights[t] > 3.0e38f) return RT_ERR_INVALID_ARG;
+        if (!valid_weight(weights[t])) return RT_ERR_INVALID_ARG;
     const int st = rt_multi_sync(m);  // frames in flight keep the bands they started with
     if (st != RT_OK) return st;
     m->weights.assign(weights, weights + n);
@@ -1257,7 +1794,7 @@ int rt_weighted_band_rows(int32_t height, int32_t nranks, int32_t rank, const fl
     // prefix sums in double, in a fixed order: every rank computes the same boundaries
     std::vector<double> P((size_t)T + 1, 0.0);
     for (int32_t t = 0; t < T; t++) {
-        if (!(weights[t] >= 0.0f)) return RT_ERR_INVALID_ARG;
+        if (!valid_weight(weights[t])) return RT_ERR_INVALID_ARG;
         P[t + 1] = P[t] + (double)weights[t];
     }
     const double total = P[T];
@@ -1324,7 +1861,12 @@ int rt_multi_render_device_frames(rt_multi* m, const rt_camera* cams, int32_t nc
         // root's receives match the senders' sends), so it depends only on what every rank
         // is given alike: the option, the frame count, the cameras (every frame the same
         // size, so the bands are fixed, and valid).  What only the root is given must then
-        // fit: at most RT_MULTI_SLOTS caller streams (one ev_in each), non-NULL buffers.
+        // fit: at most RT_MULTI_SLOTS caller streams (one ev_in each), non-NULL buffers, and
+        // a distinct buffer for every frame of a batch (frames of one batch sharing a buffer
+        // could never be whole in it: the later frame's rows would land before the earlier
+        // frame's other rows).  A refusal is returned before anything is enqueued here; with
+        // ranks in other processes their sends of this call are then unmatched, so the
+        // exchange is broken (mark_failed; the mailbox transports tell the peers).
         bool ok = true;
         for (int32_t c = 0; c < ncams && c < nframes && ok; c++)
             ok = cams[c].width == cams[0].width && cams[c].height == cams[0].height &&
@@ -1339,10 +1881,22 @@ int rt_multi_render_device_frames(rt_multi* m, const rt_camera* cams, int32_t nc
             bool bufs = true;
             for (int32_t f = 0; f < nframes && f < nbufs && bufs; f++)
                 bufs = d_frames[f] != nullptr || (size_t)cams[0].width * cams[0].height == 0;
-            if (uniq.size() > (size_t)RT_MULTI_SLOTS || !bufs) {
-                std::snprintf(m->last_err, sizeof m->last_err,
-                              "RT_OPT_MULTI_BATCH: the root takes at most %d distinct caller streams and "
-                              "non-NULL frame buffers", RT_MULTI_SLOTS);
+            const int32_t kb0 = std::min<int32_t>(m->batch, nframes);
+            std::vector<void*> dist;
+            for (int32_t f = 0; f < kb0; f++)
+                if (std::find(dist.begin(), dist.end(), d_frames[f % nbufs]) == dist.end())
+                    dist.push_back(d_frames[f % nbufs]);
+            const bool whole = (int32_t)dist.size() >= kb0 || (size_t)cams[0].width * cams[0].height == 0;
+            if (uniq.size() > (size_t)RT_MULTI_SLOTS || !bufs || !whole) {
+                if (!whole)
+                    std::snprintf(m->last_err, sizeof m->last_err,
+                                  "RT_OPT_MULTI_BATCH %d: %d distinct frame buffers for a batch of %d frames "
+                                  "(each frame of a batch needs its own buffer)", m->batch, (int)dist.size(), kb0);
+                else
+                    std::snprintf(m->last_err, sizeof m->last_err,
+                                  "RT_OPT_MULTI_BATCH: the root takes at most %d distinct caller streams and "
+                                  "non-NULL frame buffers", RT_MULTI_SLOTS);
+                if (m->nlocal < m->nranks) mark_failed(m);
                 return bufs ? RT_ERR_UNSUPPORTED : RT_ERR_INVALID_ARG;
             }
         }
@@ -1410,26 +1964,11 @@ int rt_multi_sync(rt_multi* m) {
     if (!m) return RT_ERR_INVALID_ARG;
     if (m->broken) {
         abort_comms(m);
-        for (Rank* k : m->r) {
-            DevGuard dg(k->device);
-            for (auto rs : k->render_stream) (void)hipStreamSynchronize(rs);
-            (void)hipStreamSynchronize(k->comm_stream);
-        }
+        (void)drain_streams(m, 10000);
         std::snprintf(m->last_err, sizeof m->last_err, "a frame failed after the gather was queued: communicator aborted");
         return RT_ERR_COMM;
     }
-    for (Rank* k : m->r) {
-        DevGuard dg(k->device);
-        MHIP(m, dg.err);
-        for (auto rs : k->render_stream) MHIP(m, hipStreamSynchronize(rs));
-        MHIP(m, hipStreamSynchronize(k->comm_stream));
-        if (k->comm) {
-            ncclResult_t async = ncclSuccess;
-            MNCCL(m, ncclCommGetAsyncError(k->comm, &async));
-            if (async != ncclSuccess) return nccl_err(m, async, "ncclCommGetAsyncError");
-        }
-    }
-    return RT_OK;
+    return drain_streams(m, m->timeout_ms);
 }
 
 }  // extern "C"

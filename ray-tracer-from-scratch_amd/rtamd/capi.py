@@ -33,6 +33,7 @@ RT_TRANSPORT_RCCL = 0
 RT_TRANSPORT_COPY = 1
 RT_TRANSPORT_RCCL_LOOPBACK = 2
 RT_TRANSPORT_THREADS = 3   # rehearsal: one handle per rank in one process (include/rt_capi.h)
+RT_TRANSPORT_IPC = 4       # rehearsal: one process per rank, shared-memory mailbox + HIP IPC
 RT_MULTI_ID_BYTES = 128
 RT_MULTI_SLOTS = 4
 RT_MULTI_BATCH_MAX = 16
@@ -71,6 +72,7 @@ RT_OPT_HOST_PIPELINE = 16
 RT_OPT_MULTI_FRAMES = 17
 RT_OPT_MULTI_FAULT = 18
 RT_OPT_MULTI_BATCH = 19
+RT_OPT_MULTI_TIMEOUT_MS = 20
 RT_OPT_ROW_FEEDBACK_EMA = 14
 RT_OPT_ROW_FEEDBACK_ISOLATE = 15
 

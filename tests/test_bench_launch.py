@@ -1,0 +1,100 @@
+"""bench.py's process model: `python3 bench.py --gpus N` with no
+launcher starts and supervises N ranks itself, one process per rank; a rank that fails (or
+a deadline that passes) ends the run non-zero with the rank named; WORLD_SIZE that
+disagrees with --gpus is an error.
+
+CPU: the supervisor's failure path (the children cannot run without a GPU, so each exits
+non-zero and the supervisor must report it and stop the others) and the mismatch error.
+GPU (one MI355X): the self-launched rehearsals on one GPU — 2 ranks over the torch tiler
+(gloo), 2 and 4 ranks through the native operator across processes (RT_TRANSPORT_IPC) —
+each with n_gpus = N and the gathered frames bitwise the one-GPU frame, and a fault injected
+on rank 1 ending every process non-zero."""
+import json
+import os
+import subprocess
+import sys
+import time
+
+import pytest
+
+from conftest import REPO, has_gpu
+
+BENCH = os.path.join(REPO, "bench.py")
+
+
+def _bench(args, env_extra=None, timeout=300):
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env.update(env_extra or {})
+    t0 = time.monotonic()
+    p = subprocess.run([sys.executable, BENCH] + args, env=env, capture_output=True, text=True,
+                       timeout=timeout, cwd=REPO)
+    return p, time.monotonic() - t0
+
+
+def _json(p):
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, (p.stdout[-2000:], p.stderr[-4000:])
+    return json.loads(lines[0])
+
+
+@pytest.mark.skipif(has_gpu(), reason="CPU-only: the children must fail without a GPU")
+def test_supervisor_reports_a_failed_rank_and_exits_nonzero():
+    p, dt = _bench(["--gpus", "2", "--steps", "1", "--warmup", "0", "--no-sweep",
+                    "--no-cpu-baseline", "--deadline", "120"], timeout=240)
+    assert p.returncode != 0
+    assert "bench supervisor: rank" in p.stderr and "exited with status" in p.stderr, p.stderr[-3000:]
+    assert p.stdout.strip() == ""
+
+
+def test_world_size_that_disagrees_with_gpus_is_an_error():
+    p, _ = _bench(["--gpus", "2"], env_extra={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"},
+                  timeout=120)
+    assert p.returncode == 2
+    assert "WORLD_SIZE 1" in p.stderr
+
+
+COMMON = ["--steps", "5", "--warmup", "2", "--no-sweep", "--no-cpu-baseline", "--deadline", "200"]
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not has_gpu(), reason="needs a HIP device")
+def test_self_launched_two_ranks_gloo_rehearsal():
+    """No launcher: the supervisor starts 2 ranks (torch tiler over gloo on one GPU)."""
+    p, _ = _bench(["--gpus", "2"] + COMMON, env_extra={"RT_BENCH_BACKEND": "gloo"})
+    assert p.returncode == 0, p.stderr[-4000:]
+    r = _json(p)
+    assert r["n_gpus"] == 2
+    assert r["gather_check"]["bitwise_equal_to_one_gpu_frame"] is True, r["gather_check"]
+    assert r["config"]["rehearsal"] is True
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not has_gpu(), reason="needs a HIP device")
+@pytest.mark.parametrize("n", [2, 4])
+def test_self_launched_ipc_ranks_run_the_native_operator(n):
+    """No launcher, --transport ipc: n processes on one GPU, each an rt_multi rank of the
+    native operator (bench.py's non-root branches, the id and row-weight broadcasts, the
+    batched and per-frame exchanges); every gathered buffer bitwise the one-GPU frame."""
+    p, _ = _bench(["--gpus", str(n), "--transport", "ipc"] + COMMON)
+    assert p.returncode == 0, p.stderr[-4000:]
+    r = _json(p)
+    assert r["n_gpus"] == n
+    g = r["gather_check"]
+    assert g["bitwise_equal_to_one_gpu_frame"] is True, g
+    assert g["batched"]["every_buffer_bitwise_equal"] and g["per_frame"]["every_buffer_bitwise_equal"], g
+    assert "HIP IPC" in g["operator"]
+    assert r["config"]["band_layout"] == "weighted"
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not has_gpu(), reason="needs a HIP device")
+def test_a_failed_rank_ends_the_run_nonzero():
+    """--fault-rank 1 (RT_OPT_MULTI_FAULT on rank 1, IPC transport): rank 1's frame fails
+    after its send was queued; the run ends non-zero within the deadline, rank named."""
+    p, dt = _bench(["--gpus", "2", "--transport", "ipc", "--fault-rank", "1"] + COMMON[:-2]
+                   + ["--deadline", "120"], timeout=200)
+    assert p.returncode != 0
+    assert dt < 180
+    assert "bench supervisor: rank" in p.stderr, p.stderr[-3000:]

@@ -313,6 +313,25 @@ def test_full_size_configs_vs_oracle(rend, oracle, cfg_name):
     f32, _, _ = render(rend, sc, cfg.width, cfg.height, cfg.depth, capi.RT_PREC_F32,
                        fmt=capi.RT_OUT_RGB_F32)
     check_f32(f32, o64, sig, cfg.depth, cfg_name + "/f32")
+    if cfg_name in ("c2", "c3"):
+        # the bench precision (PATH64, fp32 RGB: the frame bench.py times) against the oracle
+        # at the full headline sizes: the same segment count, EVERY pixel within the
+        # north_star's 1e-4 (main.cpp:89-119); how many exceed PATH64_TOL is reported
+        p64, sp, _ = render(rend, sc, cfg.width, cfg.height, cfg.depth, capi.RT_PREC_PATH64,
+                            fmt=capi.RT_OUT_RGB_F32, count_segments=True)
+        assert sp.segments == segs, (cfg_name, sp.segments, segs)
+        d = np.abs(p64.astype(np.float64) - o64).max(axis=-1)
+        rep = {"config": cfg_name, "pixels": int(d.size), "max_abs_delta": float(d.max()),
+               "above_2e-5": int((d > PATH64_TOL).sum()), "above_1e-4": int((d > 1e-4).sum()),
+               "above_2e-5_on_discontinuity": int(discontinuity_mask(sig)[d > PATH64_TOL].sum()),
+               "segments": int(segs)}
+        print("path64_vs_oracle", rep)
+        out = os.environ.get("RT_PARITY_REPORT")
+        if out:
+            import json
+            with open(out, "a") as fh:
+                fh.write(json.dumps(rep) + "\n")
+        assert d.max() <= 1e-4, rep
 
 
 def test_c5_sampled_rows_vs_oracle(rend, oracle):

@@ -186,6 +186,9 @@ def test_create_errors():
     uid = (C.c_uint8 * capi.RT_MULTI_ID_BYTES)()
     assert create([0], 2, 1, uid, capi.RT_TRANSPORT_COPY) == capi.RT_ERR_UNSUPPORTED
     assert create([0], 1, 1) == capi.RT_ERR_INVALID_ARG                # rank past nranks
+    assert create([0], 1, 0, uid, capi.RT_TRANSPORT_IPC) == capi.RT_ERR_INVALID_ARG  # IPC: >= 2 ranks
+    assert create([0], 2, 1, None, capi.RT_TRANSPORT_IPC) == capi.RT_ERR_INVALID_ARG  # IPC: the id
+    assert create([0], 65, 1, uid, capi.RT_TRANSPORT_IPC) == capi.RT_ERR_INVALID_ARG  # <= 64 ranks
     assert len(capi.multi_unique_id()) == capi.RT_MULTI_ID_BYTES
 
 
@@ -299,11 +302,13 @@ def test_loopback_rccl_c4_full_size_frames_in_flight(rend):
 def test_loopback_rccl_batched_gather(rend, fmt):
     """RT_OPT_MULTI_BATCH through a real (one-rank) RCCL communicator: the root renders its
     band of B frames back to back, sends them to itself in ONE ncclSend/ncclRecv pair into
-    its staging buffer and scatters them into the frames with the scatter kernel.  7 frames
-    of a moving camera over 2 buffers and 2 caller streams with B = 3 (batches 3, 3, 1) and
-    B = 16 (one batch): each buffer is bitwise the one-GPU frame of the last camera written
-    to it (the scatter keeps frame order when a batch revisits a buffer); then 9 frames of
-    one camera with B = 4 and the per-frame path (B = 1) on the same handle."""
+    its staging buffer and scatters them into the frames with the scatter kernel.  A moving
+    camera, 3 B + 1 frames over 2 B buffers on 2 caller streams (B = 3, 4; and B = 16 with 7
+    frames over 7 buffers: one batch): EVERY buffer is bitwise the one-GPU frame of the last
+    camera written to it — the third batch renders into the first one's buffers only after
+    that batch's scatter.  Too few buffers for a batch (B = 3 over 2) is refused
+    (RT_ERR_UNSUPPORTED) before anything is enqueued and the one-rank handle stays usable;
+    B = 1 (the per-frame exchange) on the same handle."""
     import torch
     dev = torch.device("cuda", 0)
     cfg = scenes.CONFIGS["c2"]
@@ -314,35 +319,35 @@ def test_loopback_rccl_batched_gather(rend, fmt):
     refs = [rend.render(c, 4, capi.RT_PREC_PATH64, 0, fmt)[0] for c in cams]
     ch = 3 if fmt == capi.RT_OUT_RGB_F32 else 1
     dt = torch.float32 if fmt == capi.RT_OUT_RGB_F32 else torch.int32
-    bufs = [torch.full((H, W, ch), -1, dtype=dt, device=dev) for _ in range(2)]
     sts = [torch.cuda.Stream(dev) for _ in range(2)]
-    nf = 7
     with capi.MultiRenderer([0], transport=capi.RT_TRANSPORT_RCCL_LOOPBACK) as m:
         m.set_scene(prims)
-        for b in (3, 16):
+        for b, nb, nf in ((3, 6, 10), (4, 8, 13), (16, 7, 7), (1, 2, 9)):
             m.set_option(capi.RT_OPT_MULTI_BATCH, b)
-            for x in bufs:
-                x.fill_(-1)
+            bufs = [torch.full((H, W, ch), -1, dtype=dt, device=dev) for _ in range(nb)]
             torch.cuda.synchronize()
             m.render_device_frames(cams, 4, [x.data_ptr() for x in bufs], capi.RT_PREC_PATH64, 0, fmt,
                                    streams=[s.cuda_stream for s in sts], nframes=nf)
             torch.cuda.synchronize()
             m.sync()
-            for i in range(2):
-                lf = max(f for f in range(nf) if f % 2 == i)
+            for i in range(nb):
+                lf = max(f for f in range(nf) if f % nb == i)
                 assert np.array_equal(bufs[i].cpu().numpy().view(np.uint32),
                                       refs[lf % len(cams)].view(np.uint32)), (b, i)
-        for b in (4, 1):
-            m.set_option(capi.RT_OPT_MULTI_BATCH, b)
-            for x in bufs:
-                x.fill_(-1)
-            torch.cuda.synchronize()
-            m.render_device_frames([cams[0]], 4, [x.data_ptr() for x in bufs], capi.RT_PREC_PATH64, 0, fmt,
-                                   streams=[s.cuda_stream for s in sts], nframes=9)
-            torch.cuda.synchronize()
-            m.sync()
-            for x in bufs:
-                assert np.array_equal(x.cpu().numpy().view(np.uint32), refs[0].view(np.uint32)), b
+            del bufs
+        m.set_option(capi.RT_OPT_MULTI_BATCH, 3)
+        two = [torch.full((H, W, ch), -1, dtype=dt, device=dev) for _ in range(2)]
+        with pytest.raises(capi.RTError) as e:
+            m.render_device_frames(cams, 4, [x.data_ptr() for x in two], capi.RT_PREC_PATH64, 0, fmt,
+                                   streams=[s.cuda_stream for s in sts], nframes=7)
+        assert e.value.status == capi.RT_ERR_UNSUPPORTED
+        # usable after the refusal: two frames (one batch of 2) into the two buffers
+        m.render_device_frames(cams[:2], 4, [x.data_ptr() for x in two], capi.RT_PREC_PATH64, 0, fmt,
+                               streams=[s.cuda_stream for s in sts], nframes=2)
+        torch.cuda.synchronize()
+        m.sync()
+        for i in range(2):
+            assert np.array_equal(two[i].cpu().numpy().view(np.uint32), refs[i].view(np.uint32)), i
         for bad in (0, capi.RT_MULTI_BATCH_MAX + 1):
             with pytest.raises(capi.RTError):
                 m.set_option(capi.RT_OPT_MULTI_BATCH, bad)
@@ -351,11 +356,12 @@ def test_loopback_rccl_batched_gather(rend, fmt):
 @pytest.mark.parametrize("W,fmt", [(96, capi.RT_OUT_RGBA8), (97, capi.RT_OUT_RGB_F64)])
 def test_batched_gather_ragged_empty_bands_and_root_limits(rend, W, fmt):
     """RT_OPT_MULTI_BATCH with ranks that have no rows (a 5-row frame over 8 THREADS handles:
-    three empty bands, which post and send nothing), batches 3 + 2 over one root buffer, in
-    RGBA8 (16-byte scatter) and, 97 pixels wide, fp64 RGB (rows not a multiple of 16 bytes:
-    the 4-byte scatter): bitwise the one-GPU frame.  And the root-only limit: a batching
+    three empty bands, which post and send nothing), batches 3 + 2 over three root buffers
+    (the second batch renders into two of the first one's buffers), in RGBA8 (16-byte
+    scatter) and, 97 pixels wide, fp64 RGB (rows not a multiple of 16 bytes: the 4-byte
+    scatter): every buffer bitwise its last frame.  And the root-only limit: a batching
     call with more than RT_MULTI_SLOTS distinct caller streams is refused
-    (RT_ERR_UNSUPPORTED) before anything is enqueued, and the handle stays usable."""
+    (RT_ERR_UNSUPPORTED) before anything is enqueued, and a one-rank handle stays usable."""
     import os
     import torch
     dev = torch.device("cuda", 0)
@@ -368,7 +374,7 @@ def test_batched_gather_ragged_empty_bands_and_root_limits(rend, W, fmt):
     uid = os.urandom(capi.RT_MULTI_ID_BYTES)
     hs = [capi.MultiRenderer([0], nranks=n, first_rank=r, unique_id=uid,
                              transport=capi.RT_TRANSPORT_THREADS) for r in range(n)]
-    buf = torch.full(shape, -1, dtype=torch.int32, device=dev)
+    bufs = [torch.full(shape, -1, dtype=torch.int32, device=dev) for _ in range(3)]
     sts = [torch.cuda.Stream(dev) for _ in range(n)]
     try:
         for h in hs:
@@ -377,14 +383,15 @@ def test_batched_gather_ragged_empty_bands_and_root_limits(rend, W, fmt):
         torch.cuda.synchronize()
 
         def drive(r, h):
-            h.render_device_frames(cams, 4, [buf.data_ptr()] if r == 0 else [], capi.RT_PREC_PATH64, 0,
-                                   fmt, streams=[sts[r].cuda_stream], nframes=5)
+            h.render_device_frames(cams, 4, [b.data_ptr() for b in bufs] if r == 0 else [],
+                                   capi.RT_PREC_PATH64, 0, fmt, streams=[sts[r].cuda_stream], nframes=5)
         errs = _run_threads(hs, drive)
         assert errs == [None] * n, errs
         torch.cuda.synchronize()
         for h in hs:
             h.sync()
-        assert np.array_equal(buf.cpu().numpy().view(np.uint32), refs[4].view(np.uint32))
+        for i, f in enumerate((3, 4, 2)):
+            assert np.array_equal(bufs[i].cpu().numpy().view(np.uint32), refs[f].view(np.uint32)), i
     finally:
         for h in hs:
             h.close()
@@ -402,6 +409,76 @@ def test_batched_gather_ragged_empty_bands_and_root_limits(rend, W, fmt):
         m.sync()
         for b in bufs[:2]:
             assert np.array_equal(b.cpu().numpy().view(np.uint32), refs[0].view(np.uint32))
+
+
+@pytest.mark.parametrize("transport", ["threads", "loopback"])
+def test_batched_frames_each_whole_in_its_own_buffer(rend, transport):
+    """B = 4 frames of a moving camera into 4 distinct buffers — every buffer
+    bitwise against ITS OWN one-GPU frame (not only the last frame written) — then 4 more
+    frames into the same 4 buffers (a batch revisiting an earlier batch's buffers), again
+    every buffer.  Over 3 THREADS handles (the process-per-GPU shape) and the one-rank
+    loopback RCCL communicator.  Then the refusal: 4 frames over 2 buffers is RT_ERR_UNSUPPORTED
+    on the root before anything is enqueued; the one-rank handle stays usable, and with
+    peers (THREADS) the exchange ends for every handle (RT_ERR_COMM, no hang)."""
+    import os
+    import torch
+    dev = torch.device("cuda", 0)
+    cfg = scenes.CONFIGS["c2"]
+    prims = scenes.to_prims(cfg.scene())
+    rend.set_scene(prims)
+    W, H = 640, 360
+    cams = [_cam(W, H, 0.02 * k) for k in range(8)]
+    refs = [rend.render(c, 4, capi.RT_PREC_PATH64, 0, capi.RT_OUT_RGB_F32)[0] for c in cams]
+    n = 3 if transport == "threads" else 1
+    if transport == "threads":
+        uid = os.urandom(capi.RT_MULTI_ID_BYTES)
+        hs = [capi.MultiRenderer([0], nranks=n, first_rank=r, unique_id=uid,
+                                 transport=capi.RT_TRANSPORT_THREADS) for r in range(n)]
+    else:
+        hs = [capi.MultiRenderer([0], transport=capi.RT_TRANSPORT_RCCL_LOOPBACK)]
+    bufs = [torch.full((H, W, 3), -1.0, device=dev) for _ in range(4)]
+    root_sts = [torch.cuda.Stream(dev) for _ in range(2)]
+    rank_sts = [torch.cuda.Stream(dev) for _ in range(n)]
+    try:
+        for h in hs:
+            h.set_scene(prims)
+            h.set_option(capi.RT_OPT_MULTI_BATCH, 4)
+        torch.cuda.synchronize()
+
+        def call(cs, ptrs):
+            def drive(r, h):
+                h.render_device_frames(cs, 4, ptrs if r == 0 else [], capi.RT_PREC_PATH64,
+                                       streams=[s.cuda_stream for s in root_sts] if r == 0
+                                       else [rank_sts[r].cuda_stream], nframes=len(cs))
+            return _run_threads(hs, drive)
+
+        for half in (cams[:4], cams[4:]):
+            errs = call(half, [b.data_ptr() for b in bufs])
+            assert errs == [None] * n, errs
+            torch.cuda.synchronize()
+            for h in hs:
+                h.sync()
+            for i in range(4):
+                want = refs[cams.index(half[i])]
+                assert np.array_equal(bufs[i].cpu().numpy().view(np.uint32), want.view(np.uint32)), i
+        errs = call(cams[:4], [b.data_ptr() for b in bufs[:2]])
+        assert isinstance(errs[0], capi.RTError) and errs[0].status == capi.RT_ERR_UNSUPPORTED, errs
+        if n > 1:
+            assert all(isinstance(e, capi.RTError) and e.status == capi.RT_ERR_COMM for e in errs[1:]), errs
+            for h in hs:
+                with pytest.raises(capi.RTError) as e:
+                    h.sync()
+                assert e.value.status == capi.RT_ERR_COMM
+        else:
+            errs = call(cams[:4], [b.data_ptr() for b in bufs])
+            assert errs == [None], errs
+            torch.cuda.synchronize()
+            hs[0].sync()
+            for i in range(4):
+                assert np.array_equal(bufs[i].cpu().numpy().view(np.uint32), refs[i].view(np.uint32)), i
+    finally:
+        for h in hs:
+            h.close()
 
 
 def test_failure_before_the_gather_is_queued_keeps_the_communicator(rend):
@@ -497,7 +574,8 @@ def test_threads_transport_runs_the_process_per_gpu_branches(rend, n, layout, fr
     already in the root's frame when its caller stream has passed the frame (checked on the
     last frame).  batch > 1 (RT_OPT_MULTI_BATCH): the batched exchange — each rank's bands of
     `batch` frames in one send, the root's one receive per rank into staging and one scatter
-    kernel per run of distinct buffers (7 frames over 2 buffers: the frames land in order);
+    kernel — over min(7, 2 x batch) root buffers (a batch needs a distinct buffer per frame;
+    a third batch revisits the first one's buffers after its scatter);
     the interleaved layout keeps the per-frame exchange.  A batched rank's caller stream
     follows its send (the part is in the root's staging; the frame rows come with the
     root's scatter), so the per-rank snapshot applies to batch 1 only."""
@@ -514,10 +592,11 @@ def test_threads_transport_runs_the_process_per_gpu_branches(rend, n, layout, fr
     uid = os.urandom(capi.RT_MULTI_ID_BYTES)
     hs = [capi.MultiRenderer([0], nranks=n, first_rank=r, unique_id=uid,
                              transport=capi.RT_TRANSPORT_THREADS) for r in range(n)]
-    bufs = [torch.full((H, W, 3), -1.0, dtype=torch.float32, device=dev) for _ in range(2)]
+    nf = 7
+    nb = 2 if batch == 1 or layout == 1 else min(nf, 2 * batch)
+    bufs = [torch.full((H, W, 3), -1.0, dtype=torch.float32, device=dev) for _ in range(nb)]
     root_sts = [torch.cuda.Stream(dev) for _ in range(2)]
     rank_sts = [torch.cuda.Stream(dev) for _ in range(n)]
-    nf = 7
     last = nf - 1
     snaps = [None] * n
     try:
@@ -542,15 +621,15 @@ def test_threads_transport_runs_the_process_per_gpu_branches(rend, n, layout, fr
             ev = torch.cuda.Event()
             ev.record(rank_sts[r])
             ev.synchronize()
-            snaps[r] = bufs[last % 2].cpu().numpy()
+            snaps[r] = bufs[last % nb].cpu().numpy()
 
         errs = _run_threads(hs, drive)
         assert errs == [None] * n, errs
         torch.cuda.synchronize()
         for h in hs:
             h.sync()
-        for b in range(2):
-            lf = max(f for f in range(nf) if f % 2 == b)
+        for b in range(nb):
+            lf = max(f for f in range(nf) if f % nb == b)
             got = bufs[b].cpu().numpy()
             assert np.array_equal(got.view(np.uint32), refs[lf % len(cams)].view(np.uint32)), (n, layout, b)
         ref_last = refs[last % len(cams)]
@@ -569,11 +648,14 @@ def test_threads_transport_runs_the_process_per_gpu_branches(rend, n, layout, fr
             h.close()
 
 
-def test_threads_transport_a_failed_rank_ends_the_exchange(rend):
+@pytest.mark.parametrize("failing", [1, 0])
+def test_threads_transport_a_failed_rank_ends_the_exchange(rend, failing):
     """A rank whose frame fails (no scene on that rank only) ends the exchange for every
-    handle: the root, already waiting for that rank's part, returns RT_ERR_COMM instead of
-    hanging; both handles are broken (later frames and rt_multi_sync: RT_ERR_COMM) and close
-    cleanly."""
+    handle: a sender's failure (failing = 1) while the root waits for its part, and a failure
+    on the root only (failing = 0, ADVICE r05: the root fails on its own rows before posting
+    its receives, while the sender is already waiting for them).  The other handle returns
+    RT_ERR_COMM instead of hanging; both are broken (later frames and rt_multi_sync:
+    RT_ERR_COMM) and close cleanly."""
     import os
     import torch
     dev = torch.device("cuda", 0)
@@ -584,19 +666,62 @@ def test_threads_transport_a_failed_rank_ends_the_exchange(rend):
     buf = torch.zeros((90, 160, 3), device=dev)
     st = torch.cuda.Stream(dev)
     try:
-        hs[0].set_scene(scenes.to_prims(scenes.synthetic_scene(8, 4)))
+        hs[1 - failing].set_scene(scenes.to_prims(scenes.synthetic_scene(8, 4)))
 
         def drive(r, h):
             h.render_device(cam, 2, buf.data_ptr() if r == 0 else 0, capi.RT_PREC_PATH64,
                             stream=st.cuda_stream if r else 0)
 
         errs = _run_threads(hs, drive)
-        assert isinstance(errs[0], capi.RTError) and errs[0].status == capi.RT_ERR_COMM, errs
-        assert isinstance(errs[1], capi.RTError) and errs[1].status == capi.RT_ERR_NO_SCENE, errs
+        other = 1 - failing
+        assert isinstance(errs[other], capi.RTError) and errs[other].status == capi.RT_ERR_COMM, errs
+        assert isinstance(errs[failing], capi.RTError) and errs[failing].status == capi.RT_ERR_NO_SCENE, errs
         for h in hs:
             with pytest.raises(capi.RTError) as e:
                 h.sync()
             assert e.value.status == capi.RT_ERR_COMM
+    finally:
+        for h in hs:
+            h.close()
+
+
+def test_sync_deadline_breaks_the_exchange_instead_of_blocking(rend):
+    """RT_OPT_MULTI_TIMEOUT_MS: rt_multi_sync polls the streams with a deadline instead of
+    blocking.  Two THREADS handles; the root's caller stream (and so its comm stream, which
+    waits on it) is held by a long queue of large renders: with a 50 ms deadline the root's
+    rt_multi_sync returns RT_ERR_COMM naming the deadline (the exchange is broken), and once
+    the GPU drains both handles close cleanly.  (No communicator here: aborting one while its
+    kernels are still queued is the RCCL path's business, not this test's.)"""
+    import os
+    import torch
+    dev = torch.device("cuda", 0)
+    cam = _cam(64, 36)
+    buf = torch.zeros((36, 64, 3), device=dev)
+    prims = scenes.to_prims(scenes.synthetic_scene(8, 4))
+    s, s1 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    uid = os.urandom(capi.RT_MULTI_ID_BYTES)
+    hs = [capi.MultiRenderer([0], nranks=2, first_rank=r, unique_id=uid,
+                             transport=capi.RT_TRANSPORT_THREADS) for r in range(2)]
+    try:
+        for h in hs:
+            h.set_scene(prims)
+        hs[0].set_option(capi.RT_OPT_MULTI_TIMEOUT_MS, 50)
+        big = torch.empty((4320, 7680, 3), device=dev)
+        rend.set_scene(scenes.to_prims(scenes.synthetic_scene(256, 0)))
+        c5 = _cam(7680, 4320)
+        for _ in range(40):
+            rend.render_device(c5, 8, big.data_ptr(), capi.RT_PREC_F64, stream=s.cuda_stream)
+
+        def drive(r, h):
+            h.render_device(cam, 2, buf.data_ptr() if r == 0 else 0, capi.RT_PREC_PATH64,
+                            stream=(s if r == 0 else s1).cuda_stream)
+
+        assert _run_threads(hs, drive) == [None, None]
+        with pytest.raises(capi.RTError) as e:
+            hs[0].sync()
+        assert e.value.status == capi.RT_ERR_COMM
+        assert "deadline" in str(e.value)
+        torch.cuda.synchronize()
     finally:
         for h in hs:
             h.close()
