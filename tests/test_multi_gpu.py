@@ -688,7 +688,7 @@ def test_threads_transport_a_failed_rank_ends_the_exchange(rend, failing):
 def test_sync_deadline_breaks_the_exchange_instead_of_blocking(rend):
     """RT_OPT_MULTI_TIMEOUT_MS: rt_multi_sync polls the streams with a deadline instead of
     blocking.  Two THREADS handles; the root's caller stream (and so its comm stream, which
-    waits on it) is held by a long queue of large renders: with a 50 ms deadline the root's
+    waits on it) is held by a long queue of GPU work: with a 50 ms deadline the root's
     rt_multi_sync returns RT_ERR_COMM naming the deadline (the exchange is broken), and once
     the GPU drains both handles close cleanly.  (No communicator here: aborting one while its
     kernels are still queued is the RCCL path's business, not this test's.)"""
@@ -706,11 +706,12 @@ def test_sync_deadline_breaks_the_exchange_instead_of_blocking(rend):
         for h in hs:
             h.set_scene(prims)
         hs[0].set_option(capi.RT_OPT_MULTI_TIMEOUT_MS, 50)
-        big = torch.empty((4320, 7680, 3), device=dev)
-        rend.set_scene(scenes.to_prims(scenes.synthetic_scene(256, 0)))
-        c5 = _cam(7680, 4320)
-        for _ in range(40):
-            rend.render_device(c5, 8, big.data_ptr(), capi.RT_PREC_F64, stream=s.cuda_stream)
+        # ~0.3 s of GPU work on the root's caller stream, enqueued in microseconds
+        a = torch.randn((8192, 8192), device=dev)
+        torch.cuda.synchronize()
+        with torch.cuda.stream(s):
+            for _ in range(40):
+                a = torch.tanh(a @ a)
 
         def drive(r, h):
             h.render_device(cam, 2, buf.data_ptr() if r == 0 else 0, capi.RT_PREC_PATH64,
