@@ -119,6 +119,8 @@ struct Rank {
     // root: batch slot b's scatter into its frames is complete (a later batch renders into
     // one of those frame buffers only after it, so every frame is whole in its buffer)
     hipEvent_t ev_bdone[2] = {};
+    // rt_multi_sync: recorded on each render stream and the comm stream, then polled
+    hipEvent_t ev_drain[RT_MULTI_SLOTS + 1] = {};
     // worker thread (local ranks other than the first, one process driving several GPUs)
     std::thread th;
     std::mutex mu;
@@ -1166,6 +1168,8 @@ void destroy_rank(Rank* k, bool abort_comm) {
         if (k->bbuf[b]) (void)hipFree(k->bbuf[b]);
         if (k->bstage[b]) (void)hipFree(k->bstage[b]);
     }
+    for (auto e : k->ev_drain)
+        if (e) (void)hipEventDestroy(e);
     for (auto& e : k->ev_ready)
         if (e) (void)hipEventDestroy(e);
     for (auto& b : k->staging)
@@ -1532,6 +1536,8 @@ int rt_multi_create(const int32_t* devices, int32_t nlocal, int32_t nranks, int3
             if (e == hipSuccess) e = hipEventRecord(k->ev_bsent[b], k->comm_stream);
             if (e == hipSuccess) e = hipEventCreateWithFlags(&k->ev_bdone[b], hipEventDisableTiming);
         }
+        for (auto& ev : k->ev_drain)
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
         if (e != hipSuccess) fail(hip_err(m, e, "rank streams/events"));
     }
     if (st == RT_OK && m->has_root()) {
@@ -1632,9 +1638,11 @@ void abort_comms(rt_multi* m) {
 }
 
 /* Waits for every local rank's streams by polling (a blocking wait could never end when a
- * peer process died with its part of the exchange outstanding): RCCL's asynchronous error is
- * checked while waiting, and when it reports one or timeout_ms (> 0) passes, the exchange is
- * broken, the communicators are aborted and RT_ERR_COMM is returned. */
+ * peer process died with its part of the exchange outstanding): an event recorded at the end
+ * of each stream is polled (hipStreamQuery was seen to report a stream done while its last
+ * command, a cross-stream wait, was still pending), RCCL's asynchronous error is checked
+ * while waiting, and when it reports one or timeout_ms (> 0) passes, the exchange is broken,
+ * the communicators are aborted and RT_ERR_COMM is returned. */
 static int drain_streams(rt_multi* m, int64_t timeout_ms) {
     const auto t0 = std::chrono::steady_clock::now();
     for (Rank* k : m->r) {
@@ -1643,12 +1651,14 @@ static int drain_streams(rt_multi* m, int64_t timeout_ms) {
         hipStream_t ss[RT_MULTI_SLOTS + 1];
         for (int s = 0; s < RT_MULTI_SLOTS; s++) ss[s] = k->render_stream[s];
         ss[RT_MULTI_SLOTS] = k->comm_stream;
-        for (hipStream_t s : ss) {
-            if (!s) continue;
+        for (int i = 0; i <= RT_MULTI_SLOTS; i++)
+            if (ss[i]) MHIP(m, hipEventRecord(k->ev_drain[i], ss[i]));
+        for (int i = 0; i <= RT_MULTI_SLOTS; i++) {
+            if (!ss[i]) continue;
             for (int it = 0;; it++) {
-                const hipError_t e = hipStreamQuery(s);
+                const hipError_t e = hipEventQuery(k->ev_drain[i]);
                 if (e == hipSuccess) break;
-                if (e != hipErrorNotReady) return hip_err(m, e, "hipStreamQuery");
+                if (e != hipErrorNotReady) return hip_err(m, e, "hipEventQuery");
                 const char* why = nullptr;
                 ncclResult_t async = ncclSuccess;
                 if (k->comm && (it & 63) == 0 && (ncclCommGetAsyncError(k->comm, &async) != ncclSuccess ||
