@@ -37,13 +37,16 @@
  * RT_TRANSPORT_IPC (rehearsal across processes): the same mailbox protocol between real
  * processes, one per rank, on one GPU or several.  The mailbox is a POSIX shared-memory
  * segment named after the unique id (one ring of posts per direction and non-root rank);
- * the root's staging buffers and every rank's exchange events are shared with
- * hipIpcGetMemHandle / hipIpcGetEventHandle once, at create (staging buffers again when they
- * grow).  A sender's comm stream waits on the root's imported "ready" event, copies its
- * part into the root's staging buffer through the imported mapping and records its own
- * "sent" event, which the root's comm stream waits on before copying the part into the
- * frame rows.  So bench.py's process-per-GPU code (its non-root branches, the broadcasts of
- * the id and the row weights) runs in separate processes on a one-GPU box.
+ * the root's staging buffers are shared with hipIpcGetMemHandle (once per allocation).  The
+ * cross-process stream ordering uses two sequence counters per rank in the same segment,
+ * set and awaited ON the streams by host functions (hipLaunchHostFunc): the root's comm
+ * stream sets "ready" once the destination may be written; the sender's comm stream waits
+ * for it, copies its part into the root's staging buffer through the imported mapping and
+ * sets "sent"; the root's comm stream waits for that before copying the part into the frame
+ * rows.  (HIP's own IPC events were used first: after ~1,000 frames a wait on an imported
+ * event failed with "invalid argument", so the ordering is now this file's own.)  So
+ * bench.py's process-per-GPU code (its non-root branches, the broadcasts of the id and the
+ * row weights) runs in separate processes on a one-GPU box.
  */
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -158,7 +161,8 @@ std::map<std::string, std::shared_ptr<Hub>> g_hubs;
  * where g's part of a frame/batch lands) and `sent` (g posts that its copy was enqueued). */
 constexpr int IPC_MAX_RANKS = 64;
 constexpr int IPC_RING = 16;
-// the exchange events every rank exports: ev_ready[slot] (root), ev_sent[slot], ev_bsent[b]
+// the exchange events of a rank by index (THREADS posts name one): ev_ready[slot] (root),
+// ev_sent[slot], ev_bsent[b]
 enum : int { EV_READY = 0, EV_SENT = RT_MULTI_SLOTS, EV_BSENT = 2 * RT_MULTI_SLOTS, IPC_NEV = EV_BSENT + 2 };
 struct IpcMsg {
     uint64_t seq;       // n + 1 once message n of the ring is written (release)
@@ -172,10 +176,13 @@ struct IpcRing {
     uint64_t taken;     // messages consumed (release)
 };
 struct IpcPeer {
-    uint32_t joined, left;  // set once (release): handles written / imports closed
+    uint32_t joined, left;  // set once (release): joined / its imports closed
     int32_t pid, nranks;
-    hipIpcEventHandle_t ev[IPC_NEV];
-    IpcRing recv, sent;
+    // stream-order counters for this (non-root) rank's posts, set by host functions on the
+    // streams: ready = post n's destination may be written (root), sent = post n's copy has
+    // landed (sender); value n + 1
+    uint64_t ready, sent;
+    IpcRing recv, sent_ring;
 };
 struct IpcShared {
     uint32_t failed;        // a handle failed mid-exchange: every wait gives up
@@ -186,7 +193,6 @@ struct Ipc {
     IpcShared* sh = nullptr;
     std::string name;
     bool unlinked = false, joined = false;
-    std::vector<std::array<hipEvent_t, IPC_NEV>> imp;  // the peers' events opened here
     struct Exp {
         void* base;
         size_t bytes;
@@ -451,6 +457,45 @@ int ipc_take(rt_multi* m, IpcRing& r, uint64_t& count, uint64_t frame, IpcMsg* o
     }
     return RT_OK;
 }
+/* Stream-ordered counters in the shared segment (the IPC transport's events): a host
+ * function on a stream sets *word = value once the stream's earlier work is done, or holds
+ * the stream until *word >= value (a handle's failure, or the transport timeout, releases
+ * it: the exchange is broken by then and the frame's contents are not used). */
+struct SeqOp {
+    uint64_t* word;
+    uint64_t value;
+    const uint32_t* failed;
+    int64_t timeout_ms;
+};
+void seq_set_fn(void* a) {
+    SeqOp* o = static_cast<SeqOp*>(a);
+    st_rel(o->word, o->value);
+    delete o;
+}
+void seq_wait_fn(void* a) {
+    SeqOp* o = static_cast<SeqOp*>(a);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int it = 0; ld_acq(o->word) < o->value && !ld_acq(o->failed); it++) {
+        if (it < 4096) {
+            std::this_thread::yield();
+        } else {
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(o->timeout_ms)) break;
+            std::this_thread::sleep_for(std::chrono::microseconds(20));
+        }
+    }
+    delete o;
+}
+int seq_enqueue(rt_multi* m, hipStream_t st, uint64_t* word, uint64_t value, bool wait) {
+    SeqOp* o = new (std::nothrow) SeqOp{word, value, &m->ipc->sh->failed, hub_timeout_ms()};
+    if (!o) return RT_ERR_OUT_OF_MEMORY;
+    const hipError_t e = hipLaunchHostFunc(st, wait ? seq_wait_fn : seq_set_fn, o);
+    if (e != hipSuccess) {
+        delete o;
+        return hip_err(m, e, "hipLaunchHostFunc");
+    }
+    return RT_OK;
+}
+
 /* A staging buffer of the root that senders write into: hipMalloc'd and exported once; kept
  * until destroy (a peer may still hold the mapping when it grows). */
 int ipc_alloc(rt_multi* m, size_t bytes, void** out) {
@@ -505,6 +550,9 @@ int mbox_post_recv(rt_multi* m, Rank* k, uint64_t frame, int g, char* dst, size_
     v.alloc = a->id;
     v.ev = ev_idx;
     v.mem = a->h;
+    // "ready" for this post once the root's comm stream (where ev_idx was recorded) is here
+    const int st = seq_enqueue(m, k->comm_stream, &x.sh->peer[g].ready, x.nrecv[g] + 1, false);
+    if (st != RT_OK) return st;
     return ipc_post(m, x.sh->peer[g].recv, x.nrecv[g], v, g, "posting a receive");
 }
 /* Sender: where this rank's part of `frame` goes (*dst on device *dev); `st` waits until it
@@ -540,12 +588,8 @@ int mbox_take_recv(rt_multi* m, Rank* k, uint64_t frame, size_t bytes, hipStream
     }
     *dst = static_cast<char*>(it->second) + v.offset;
     *dev = k->device;
-    if (!x.imp[0][v.ev]) {
-        std::snprintf(m->last_err, sizeof m->last_err, "IPC: the root posted event %d, not imported", v.ev);
-        return RT_ERR_COMM;
-    }
-    MHIPF(m, hipStreamWaitEvent(st, x.imp[0][v.ev], 0));
-    return RT_OK;
+    // the stream waits for the root's "ready" of this post (ipc_take advanced the count)
+    return seq_enqueue(m, st, &x.sh->peer[k->rank].ready, x.nrecv_taken, true);
 }
 /* Sender: this rank's copy of `frame`'s part is complete once its event ev_idx fires. */
 int mbox_post_sent(rt_multi* m, Rank* k, uint64_t frame, int ev_idx) {
@@ -560,7 +604,10 @@ int mbox_post_sent(rt_multi* m, Rank* k, uint64_t frame, int ev_idx) {
     IpcMsg v{};
     v.frame = frame;
     v.ev = ev_idx;
-    return ipc_post(m, x.sh->peer[k->rank].sent, x.nsent_posted, v, 0, "posting a send");
+    // "sent" for this post once this rank's comm stream (its copy) is here
+    const int st = seq_enqueue(m, k->comm_stream, &x.sh->peer[k->rank].sent, x.nsent_posted + 1, false);
+    if (st != RT_OK) return st;
+    return ipc_post(m, x.sh->peer[k->rank].sent_ring, x.nsent_posted, v, 0, "posting a send");
 }
 /* Root: `st` waits until rank g's part of `frame` has landed. */
 int mbox_take_sent(rt_multi* m, Rank* k, uint64_t frame, int g, hipStream_t st) {
@@ -571,14 +618,9 @@ int mbox_take_sent(rt_multi* m, Rank* k, uint64_t frame, int g, hipStream_t st) 
     }
     Ipc& x = *m->ipc;
     IpcMsg v{};
-    const int e = ipc_take(m, x.sh->peer[g].sent, x.nsent[g], frame, &v, g, "waiting for a part's copy");
+    const int e = ipc_take(m, x.sh->peer[g].sent_ring, x.nsent[g], frame, &v, g, "waiting for a part's copy");
     if (e != RT_OK) return e;
-    if (!x.imp[g][v.ev]) {
-        std::snprintf(m->last_err, sizeof m->last_err, "IPC: rank %d posted event %d, not imported", g, v.ev);
-        return RT_ERR_COMM;
-    }
-    MHIPF(m, hipStreamWaitEvent(st, x.imp[g][v.ev], 0));
-    return RT_OK;
+    return seq_enqueue(m, st, &x.sh->peer[g].sent, x.nsent[g], true);
 }
 /* A sender's copy into the destination mbox_take_recv returned. */
 int mbox_copy(rt_multi* m, Rank* k, char* dst, int dev, const void* src, size_t bytes, hipStream_t st) {
@@ -1213,9 +1255,7 @@ void mark_failed(rt_multi* m) {
 }
 
 /* ---- RT_TRANSPORT_IPC setup and teardown ---- */
-/* Opens (or creates) the id's segment, exports this rank's exchange events, waits until every
- * rank has joined and imports the peers' events it waits on (root: every sender's sent
- * events; a sender: the root's ready events). */
+/* Opens (or creates) the id's segment and waits until every rank has joined. */
 int ipc_create(rt_multi* m, const uint8_t* id) {
     m->ipc.reset(new (std::nothrow) Ipc());
     if (!m->ipc) return RT_ERR_OUT_OF_MEMORY;
@@ -1239,7 +1279,6 @@ int ipc_create(rt_multi* m, const uint8_t* id) {
         return RT_ERR_COMM;
     }
     x.sh = static_cast<IpcShared*>(p);
-    x.imp.assign((size_t)m->nranks, std::array<hipEvent_t, IPC_NEV>{});
     x.nrecv.assign((size_t)m->nranks, 0);
     x.nsent.assign((size_t)m->nranks, 0);
     Rank* k = m->r[0];
@@ -1250,7 +1289,6 @@ int ipc_create(rt_multi* m, const uint8_t* id) {
         std::snprintf(m->last_err, sizeof m->last_err, "IPC: rank %d joined %s twice", k->rank, name);
         return RT_ERR_INVALID_ARG;
     }
-    for (int i = 0; i < IPC_NEV; i++) MHIP(m, hipIpcGetEventHandle(&me.ev[i], local_ev(k, i)));
     me.pid = (int32_t)::getpid();
     me.nranks = m->nranks;
     st_rel(&me.joined, 1u);
@@ -1268,30 +1306,20 @@ int ipc_create(rt_multi* m, const uint8_t* id) {
             return RT_ERR_INVALID_ARG;
         }
     if (m->has_root()) {
-        for (int g = 1; g < m->nranks; g++)
-            for (int i = EV_SENT; i < IPC_NEV; i++)
-                MHIP(m, hipIpcOpenEventHandle(&x.imp[g][i], x.sh->peer[g].ev[i]));
         // every rank has the segment mapped: drop its name (nothing left in /dev/shm)
         ::shm_unlink(name);
         x.unlinked = true;
-    } else {
-        for (int i = EV_READY; i < EV_SENT; i++) MHIP(m, hipIpcOpenEventHandle(&x.imp[0][i], x.sh->peer[0].ev[i]));
     }
     return RT_OK;
 }
-/* Before this rank's exported events and buffers are destroyed: close what it imported, mark
- * it left, and wait (bounded) until every peer has done the same, so no peer still uses them. */
+/* Before this rank's exported buffers are freed (and the segment unmapped): close what it
+ * imported, mark it left, and wait (bounded) until every peer has done the same, so no peer
+ * still uses them.  The streams were drained first, so no host function still runs. */
 void ipc_leave(rt_multi* m) {
     if (!m->ipc) return;
     Ipc& x = *m->ipc;
     if (x.sh) {
         DevGuard dg(m->r.empty() ? 0 : m->r[0]->device);
-        for (auto& a : x.imp)
-            for (auto& e : a)
-                if (e) {
-                    (void)hipEventDestroy(e);
-                    e = nullptr;
-                }
         for (auto& o : x.opened) (void)hipIpcCloseMemHandle(o.second);
         x.opened.clear();
         if (x.joined && !m->r.empty()) {
@@ -1516,8 +1544,7 @@ int rt_multi_create(const int32_t* devices, int32_t nlocal, int32_t nranks, int3
         }
         DevGuard dg(k->device);
         hipError_t e = dg.err;
-        // the events a peer process waits on (IPC): shareable with hipIpcGetEventHandle
-        const unsigned xf = hipEventDisableTiming | (transport == RT_TRANSPORT_IPC ? hipEventInterprocess : 0u);
+        const unsigned xf = hipEventDisableTiming;
         for (auto& rs : k->render_stream)
             if (e == hipSuccess) e = hipStreamCreateWithFlags(&rs, hipStreamNonBlocking);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&k->comm_stream, hipStreamNonBlocking);
@@ -1575,12 +1602,7 @@ int rt_multi_create(const int32_t* devices, int32_t nlocal, int32_t nranks, int3
         std::lock_guard<std::mutex> lk2(h->mu);
         h->refs++;
     }
-    if (st == RT_OK && transport == RT_TRANSPORT_IPC) {
-        // the events recorded above must be in the runtime before a peer opens them
-        DevGuard dg(m->r[0]->device);
-        if (hipStreamSynchronize(m->r[0]->comm_stream) != hipSuccess) fail(RT_ERR_HIP);
-        else fail(ipc_create(m, unique_id));
-    }
+    if (st == RT_OK && transport == RT_TRANSPORT_IPC) fail(ipc_create(m, unique_id));
     // one rank: the band is the frame and nothing is exchanged, so no communicator (RCCL's
     // init would only print its banner on stdout and start its proxy thread) — except for
     // the loopback transport, whose root sends its band to itself

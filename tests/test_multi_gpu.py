@@ -705,6 +705,16 @@ def test_sync_deadline_breaks_the_exchange_instead_of_blocking(rend):
     try:
         for h in hs:
             h.set_scene(prims)
+
+        def drive(r, h):
+            h.render_device(cam, 2, buf.data_ptr() if r == 0 else 0, capi.RT_PREC_PATH64,
+                            stream=(s if r == 0 else s1).cuda_stream)
+
+        # one frame first: its lazy allocations (band buffers, per-stream state) may wait on
+        # the device, which must happen before the hold below
+        assert _run_threads(hs, drive) == [None, None]
+        for h in hs:
+            h.sync()
         hs[0].set_option(capi.RT_OPT_MULTI_TIMEOUT_MS, 50)
         # ~0.3 s of GPU work on the root's caller stream, enqueued in microseconds
         a = torch.randn((8192, 8192), device=dev)
@@ -712,11 +722,6 @@ def test_sync_deadline_breaks_the_exchange_instead_of_blocking(rend):
         with torch.cuda.stream(s):
             for _ in range(40):
                 a = torch.tanh(a @ a)
-
-        def drive(r, h):
-            h.render_device(cam, 2, buf.data_ptr() if r == 0 else 0, capi.RT_PREC_PATH64,
-                            stream=(s if r == 0 else s1).cuda_stream)
-
         assert _run_threads(hs, drive) == [None, None]
         with pytest.raises(capi.RTError) as e:
             hs[0].sync()
