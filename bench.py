@@ -931,7 +931,10 @@ def main(argv=None) -> int:
         flops = my_segs * flop_per_segment(n_sph, n_wall)
         valu_peak = VALU_PEAK_TFLOPS[args.precision]
         if tiled_mode:
-            par = (f"row-tiled x{world} + gather ({'RCCL send/recv, rt_multi' if multi is not None else 'torch.distributed ' + backend})"
+            gname = ({"rccl": "RCCL send/recv, rt_multi", "ipc": "HIP IPC copies, rt_multi (rehearsal)",
+                      "copy": "peer copies, rt_multi"}[args.transport] if multi is not None
+                     else "torch.distributed " + backend)
+            par = (f"row-tiled x{world} + gather ({gname})"
                    if world > 1 else "one GPU (the one band is the whole frame)")
             if args.local_ranks > 1:
                 par = f"REHEARSAL: {args.local_ranks} ranks on one GPU, peer copies"
