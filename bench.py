@@ -275,6 +275,9 @@ def main(argv=None) -> int:
                     help="N > 1: frames per gather (RT_OPT_MULTI_BATCH): each rank sends its bands "
                          "of that many frames in one ncclSend, the root scatters them with one "
                          "kernel (the per-frame exchange's host calls cost more than a 1/8 band)")
+    ap.add_argument("--frame-batch", type=int, default=0,
+                    help="RT_OPT_FRAME_BATCH: a rank's band frames of one gather go to the GPU as "
+                         "one launch (0 = auto: the gather's batch at N > 1, else 1)")
     ap.add_argument("--local-ranks", type=int, default=1,
                     help="rehearsal only (one process): split the frame over this many ranks "
                          "on this one GPU with the peer-copy transport; not a measurement")
@@ -399,6 +402,8 @@ def main(argv=None) -> int:
     torch.cuda.set_stream(stream)
     st_ptrs = [s_.cuda_stream for s_ in streams]
     rank_batch = max(1, min(capi.RT_MULTI_BATCH_MAX, args.rank_batch))
+    frame_batch = max(1, min(capi.RT_MULTI_BATCH_MAX,
+                             args.frame_batch if args.frame_batch > 0 else rank_batch))
     # frame buffers: the whole frame on rank 0 (tiled: the bands are gathered into it) or on
     # every rank (frames mode); fp32-RGB sized, which the sweep below also writes.  The
     # batched exchange (N > 1) needs a distinct buffer per frame of a batch (rt_capi.h
@@ -456,6 +461,7 @@ def main(argv=None) -> int:
         if multi.nranks > 1:
             multi.set_option(capi.RT_OPT_MULTI_FRAMES, max(1, min(capi.RT_MULTI_SLOTS, args.rank_frames)))
             multi.set_option(capi.RT_OPT_MULTI_BATCH, rank_batch)
+            multi.set_option(capi.RT_OPT_FRAME_BATCH, frame_batch)
     elif tiled_mode:
         from rtamd import tiling
         # double-buffered: the gather of frame k (collective stream) overlaps the render of k+1
@@ -969,6 +975,7 @@ def main(argv=None) -> int:
                 "band_layout": args.band_layout if (tiled_mode and (world > 1 or args.local_ranks > 1)) else None,
                 "rank_frames_in_flight": args.rank_frames if (tiled_mode and (world > 1 or args.local_ranks > 1)) else None,
                 "frames_per_gather": args.rank_batch if (tiled_mode and world > 1) else None,
+                "frames_per_launch": frame_batch if (multi is not None and multi.nranks > 1) else 1,
                 "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
                 "host_box_cache": bool(args.box_cache),
                 "row_feedback": args.row_feedback,

@@ -214,6 +214,20 @@ enum rt_option {
                                          calling thread launches the current frame; 0 = one
                                          thread does both in turn.  The same launches in the
                                          same order: output is identical. */
+    RT_OPT_FRAME_BATCH = 21,         /* B in [1, RT_MULTI_BATCH_MAX] (default 1): in
+                                         rt_render_device_frames with the host pipeline,
+                                         up to B consecutive frames on the same stream that
+                                         write distinct buffers go to the GPU as ONE launch
+                                         (frame = blockIdx.z; each frame's kernel arguments
+                                         in a device table copied in front of the launch),
+                                         so the host pays one launch per group instead of
+                                         one per frame.  Frames sampled by
+                                         RT_OPT_ROW_FEEDBACK, a change of the row order's
+                                         grid, wave-cull scenes and RT_OPT_PIXEL_PAIRS launch
+                                         one frame at a time.  On rt_multi_set_option: also
+                                         a rank renders its batch's bands (and the root its
+                                         rows) on one stream, so RT_OPT_MULTI_BATCH's band
+                                         frames become one launch.  Output is identical. */
     RT_OPT_MULTI_FRAMES = 17,        /* rt_multi_set_option only: F in [1, RT_MULTI_SLOTS]
                                          (default 2) band slots per rank — frames of a rank in
                                          flight on F render streams, so a small band's longest

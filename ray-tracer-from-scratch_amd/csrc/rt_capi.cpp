@@ -177,6 +177,18 @@ struct rt_ctx {
     bool host_pipeline = true;
     struct Prep;
     Prep* prep = nullptr;
+    // RT_OPT_FRAME_BATCH: the pipelined frame loop launches up to frame_batch consecutive
+    // frames that share a stream as ONE grid (frame = blockIdx.z, rt::launch_trace_batch),
+    // their kernel arguments in a device table copied from pinned memory in front of the
+    // launch.  TAB_SLOTS groups may be in flight; a slot is reused once its launch (whose
+    // stop event is tab_ev[slot]) has completed.
+    int frame_batch = 1;
+    static constexpr int TAB_SLOTS = 16;
+    rt::KParams* h_tab = nullptr;  // pinned, TAB_SLOTS x RT_MULTI_BATCH_MAX
+    rt::KParams* d_tab = nullptr;  // device, the same
+    hipEvent_t tab_ev[TAB_SLOTS] = {};
+    bool tab_busy[TAB_SLOTS] = {};
+    int tab_next = 0;
     char last_err[256] = {0};
 };
 
@@ -246,6 +258,11 @@ int launch_event(rt_ctx* ctx, hipStream_t st, hipEvent_t* ev) {
 int wait_inflight(rt_ctx* ctx) {
     if (ctx->stream) RT_HIP(ctx, hipStreamSynchronize(ctx->stream));
     for (auto& f : ctx->inflight) RT_HIP(ctx, hipEventSynchronize(f.ev));
+    for (int s = 0; s < rt_ctx::TAB_SLOTS; s++)  // batched launches (RT_OPT_FRAME_BATCH)
+        if (ctx->tab_busy[s]) {
+            RT_HIP(ctx, hipEventSynchronize(ctx->tab_ev[s]));
+            ctx->tab_busy[s] = false;
+        }
     return RT_OK;
 }
 
@@ -1163,6 +1180,10 @@ int rt_ctx_destroy(rt_ctx* ctx) {
     (void)wait_inflight(ctx);  // frames in flight on caller streams still read the scene
     for (auto& f : ctx->inflight) (void)hipEventDestroy(f.ev);
     ctx->inflight.clear();
+    for (auto& e : ctx->tab_ev)
+        if (e) (void)hipEventDestroy(e);
+    if (ctx->d_tab) (void)hipFree(ctx->d_tab);
+    if (ctx->h_tab) (void)hipHostFree(ctx->h_tab);
     if (ctx->d_scene) (void)hipFree(ctx->d_scene);
     if (ctx->d_out) (void)hipFree(ctx->d_out);
     if (ctx->d_segs) (void)hipFree(ctx->d_segs);
@@ -1279,6 +1300,10 @@ int rt_set_option(rt_ctx* ctx, int32_t option, int64_t value) {
         case RT_OPT_HOST_PIPELINE:
             if (value != 0 && value != 1) return RT_ERR_INVALID_ARG;
             ctx->host_pipeline = value == 1;
+            return RT_OK;
+        case RT_OPT_FRAME_BATCH:
+            if (value < 1 || value > RT_MULTI_BATCH_MAX) return RT_ERR_INVALID_ARG;
+            ctx->frame_batch = (int)value;
             return RT_OK;
         case RT_OPT_ROW_FEEDBACK_ISOLATE:
             if (value != 0 && value != 1) return RT_ERR_INVALID_ARG;
@@ -1568,6 +1593,37 @@ static int32_t interleaved_rows(int32_t height, int32_t nparts, int32_t part) {
     return n;
 }
 
+/* One frame whose arguments are complete (prepare_rows done): the stream's in-flight event,
+ * the isolation waits, the launch, the cost snapshot of a sampled frame. */
+static int launch_prepared(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nrows,
+                           const rt::KParams& p, int32_t precision, hipStream_t hs,
+                           double* hp = nullptr) {
+#if RT_HOST_PROFILE
+    double hp_local = hp ? *hp : hp_now();
+    double& hp_t = hp ? *hp : hp_local;
+#else
+    (void)hp;
+#endif
+    hipEvent_t done = nullptr;
+    int st = launch_event(ctx, hs, &done);
+    if (st != RT_OK) return st;
+    const bool sampled = p.tile_cost != nullptr;
+    st = isolate_before(ctx, hs, sampled);
+    if (st != RT_OK) return st;
+    HP(2);
+    // RT_DRY_LAUNCH (diagnostic builds, tools/multi_host_cost.py): every host step of the
+    // frame but the kernel launch, to separate the host's own work from the runtime's
+    const int e = RT_DRY_LAUNCH ? (int)hipSuccess : rt::launch_trace(p, precision, hs, done);
+    if (e != (int)hipSuccess) return hip_fail(ctx, (hipError_t)e, "launch k_trace");
+    if (RT_DRY_LAUNCH) return RT_OK;
+    st = isolate_after(ctx, hs, sampled);
+    if (st != RT_OK) return st;
+    HP(3);
+    st = snapshot_costs(ctx, cam, row0, nrows, hs, p);
+    HP(4);
+    return st;
+}
+
 /* rt_render_device and rt_render_device_interleaved: a contiguous band [row0, row0 + nrows)
  * (nparts == 0) or interleaved part `part` of `nparts` (nrows = its pixel rows). */
 static int render_device_impl(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nrows,
@@ -1609,24 +1665,11 @@ static int render_device_impl(rt_ctx* ctx, const rt_camera* cam, int32_t row0, i
     hipStream_t hs = static_cast<hipStream_t>(s);
     st = prepare_rows(ctx, cam, row0, nrows, hs, p);
     if (st != RT_OK) return st;
-    hipEvent_t done = nullptr;
-    st = launch_event(ctx, hs, &done);
-    if (st != RT_OK) return st;
-    const bool sampled = p.tile_cost != nullptr;
-    st = isolate_before(ctx, hs, sampled);
-    if (st != RT_OK) return st;
-    HP(2);
-    // RT_DRY_LAUNCH (diagnostic builds, tools/multi_host_cost.py): every host step of the
-    // frame but the kernel launch, to separate the host's own work from the runtime's
-    const int e = RT_DRY_LAUNCH ? (int)hipSuccess : rt::launch_trace(p, precision, s, done);
-    if (e != (int)hipSuccess) return hip_fail(ctx, (hipError_t)e, "launch k_trace");
-    if (RT_DRY_LAUNCH) return RT_OK;
-    st = isolate_after(ctx, hs, sampled);
-    if (st != RT_OK) return st;
-    HP(3);
-    st = snapshot_costs(ctx, cam, row0, nrows, hs, p);
-    HP(4);
-    return st;
+#if RT_HOST_PROFILE
+    return launch_prepared(ctx, cam, row0, nrows, p, precision, hs, &hp_t);
+#else
+    return launch_prepared(ctx, cam, row0, nrows, p, precision, hs);
+#endif
 }
 
 int rt_render_device(rt_ctx* ctx, const rt_camera* cam, int32_t row0, int32_t nrows,
@@ -1655,6 +1698,92 @@ int rt_render_device_interleaved(rt_ctx* ctx, const rt_camera* cam, int32_t npar
     return render_device_impl(ctx, cam, 0, interleaved_rows(cam->height, nparts, part), nparts,
                               part, out_frame_rows, depth, precision, flags, out_format, d_out,
                               d_segments, stream);
+}
+
+/* RT_OPT_FRAME_BATCH: a group of n >= 2 prepared frames of one stream (their arguments in
+ * the pinned table slot s) as one launch — the slot copied into the device table behind the
+ * stream's earlier work, then one grid of n frames whose stop event marks the slot free
+ * again; n == 1 is an ordinary launch. */
+static int launch_group(rt_ctx* ctx, int s, int n, const rt_camera* cam, int32_t row0, int32_t nrows,
+                        int32_t precision, hipStream_t hs) {
+    if (n <= 0) return RT_OK;
+    rt::KParams* grp = ctx->h_tab + (size_t)s * RT_MULTI_BATCH_MAX;
+    if (n == 1) return launch_prepared(ctx, cam, row0, nrows, grp[0], precision, hs);
+    int st = isolate_before(ctx, hs, false);
+    if (st != RT_OK) return st;
+    rt::KParams* dst = ctx->d_tab + (size_t)s * RT_MULTI_BATCH_MAX;
+    RT_HIP(ctx, hipMemcpyAsync(dst, grp, (size_t)n * sizeof(rt::KParams), hipMemcpyHostToDevice, hs));
+    const int e = RT_DRY_LAUNCH ? (int)hipSuccess
+                                : rt::launch_trace_batch(dst, grp[0], n, precision, hs, ctx->tab_ev[s]);
+    if (e != (int)hipSuccess) return hip_fail(ctx, (hipError_t)e, "launch k_trace_tab");
+    ctx->tab_busy[s] = !RT_DRY_LAUNCH;
+    ctx->tab_next = (s + 1) % rt_ctx::TAB_SLOTS;
+    return RT_OK;
+}
+
+/* The pipelined frame loop with RT_OPT_FRAME_BATCH: consecutive frames are grouped while they
+ * share a stream (frames on one stream run in order anyway), write distinct buffers, have
+ * the same grid (a row order change between them starts a new group) and are not sampled by
+ * the row feedback (a sampled frame runs alone, through the stamped kernels, then its cost
+ * snapshot); each group is one launch.  Every frame's arguments, row order and feedback
+ * bookkeeping are the per-frame loop's, so the output is identical. */
+static int launch_frame_groups(rt_ctx* ctx, const rt_camera* cams, int32_t ncams, int32_t row0,
+                               int32_t nrows, int32_t precision, void* const* d_outs, int32_t nouts,
+                               void* const* streams, int32_t nstreams, int32_t nframes) {
+    rt_ctx::Prep& q = *ctx->prep;
+    DeviceGuard dg(ctx->device);
+    RT_HIP(ctx, dg.err);
+    if (!ctx->d_tab) {
+        const size_t n = (size_t)rt_ctx::TAB_SLOTS * RT_MULTI_BATCH_MAX;
+        for (auto& e : ctx->tab_ev)
+            if (!e) RT_HIP(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        if (!ctx->h_tab) RT_HIP(ctx, hipHostMalloc(&ctx->h_tab, n * sizeof(rt::KParams), hipHostMallocDefault));
+        RT_HIP(ctx, hipMalloc(&ctx->d_tab, n * sizeof(rt::KParams)));
+    }
+    int st = RT_OK;
+    int32_t f = 0;
+    while (f < nframes && st == RT_OK) {
+        void* const stf = nstreams > 0 ? streams[f % nstreams] : nullptr;
+        hipStream_t hs = static_cast<hipStream_t>(stf ? stf : static_cast<void*>(ctx->stream));
+        const int s = ctx->tab_next;  // this group's table slot: free once its last launch ended
+        if (ctx->tab_busy[s]) {
+            RT_HIP(ctx, hipEventSynchronize(ctx->tab_ev[s]));
+            ctx->tab_busy[s] = false;
+        }
+        rt::KParams* grp = ctx->h_tab + (size_t)s * RT_MULTI_BATCH_MAX;
+        const void* outs[RT_MULTI_BATCH_MAX];
+        int n = 0;
+        const rt_camera* cam0 = &cams[f % ncams];
+        while (f < nframes && n < ctx->frame_batch) {
+            void* const st2 = nstreams > 0 ? streams[f % nstreams] : nullptr;
+            void* const out = d_outs[f % nouts];
+            if (n > 0 && (st2 != stf || std::find(outs, outs + n, out) != outs + n)) break;
+            while (q.produced.load(std::memory_order_acquire) <= f) std::this_thread::yield();
+            rt::KParams& p = grp[n];
+            p = q.slot[f % rt_ctx::Prep::RING];
+            q.consumed.store(f + 1, std::memory_order_release);
+            const rt_camera* cam = &cams[f % ncams];
+            st = prepare_rows(ctx, cam, row0, nrows, hs, p);
+            if (st != RT_OK) break;
+            const bool other_grid = n > 0 && (p.W != grp[0].W || p.nrows != grp[0].nrows ||
+                                              p.row_units_log2 != grp[0].row_units_log2);
+            if (p.tile_cost || other_grid) {
+                // this frame alone (after the frames grouped so far), through the per-frame path
+                const rt::KParams one = p;
+                st = launch_group(ctx, s, n, cam0, row0, nrows, precision, hs);
+                if (st == RT_OK) st = launch_prepared(ctx, cam, row0, nrows, one, precision, hs);
+                n = 0;
+                f++;
+                break;
+            }
+            outs[n++] = out;
+            f++;
+        }
+        if (st == RT_OK) st = launch_group(ctx, s, n, cam0, row0, nrows, precision, hs);
+    }
+    // the helper thread must not wait for a consumer that stopped early
+    q.consumed.store(nframes, std::memory_order_release);
+    return st;
 }
 
 /* rt_render_device_frames with the host pipeline (RT_OPT_HOST_PIPELINE): the helper thread
@@ -1699,14 +1828,19 @@ static int render_frames_pipelined(rt_ctx* ctx, const rt_camera* cams, int32_t n
     }
     q.cv.notify_one();
     int st = RT_OK;
-    for (int32_t f = 0; f < nframes; f++) {
-        while (q.produced.load(std::memory_order_acquire) <= f) std::this_thread::yield();
-        void* stf = nstreams > 0 ? streams[f % nstreams] : nullptr;
-        st = render_device_impl(ctx, &cams[f % ncams], row0, nrows, 0, 0, 0, depth, precision, flags,
-                                out_format, d_outs[f % nouts], nullptr, stf,
-                                &q.slot[f % rt_ctx::Prep::RING]);
-        q.consumed.store(f + 1, std::memory_order_release);
-        if (st != RT_OK) break;
+    if (ctx->frame_batch > 1) {
+        st = launch_frame_groups(ctx, cams, ncams, row0, nrows, precision, d_outs, nouts, streams,
+                                 nstreams, nframes);
+    } else {
+        for (int32_t f = 0; f < nframes; f++) {
+            while (q.produced.load(std::memory_order_acquire) <= f) std::this_thread::yield();
+            void* stf = nstreams > 0 ? streams[f % nstreams] : nullptr;
+            st = render_device_impl(ctx, &cams[f % ncams], row0, nrows, 0, 0, 0, depth, precision, flags,
+                                    out_format, d_outs[f % nouts], nullptr, stf,
+                                    &q.slot[f % rt_ctx::Prep::RING]);
+            q.consumed.store(f + 1, std::memory_order_release);
+            if (st != RT_OK) break;
+        }
     }
     // the helper is done with this batch before its arguments (cams, d_outs) go out of scope
     q.stop.store(true, std::memory_order_release);

@@ -222,6 +222,12 @@ static_assert(sizeof(KParams) <= 16384, "kernel arguments over 16 KB");
 // hipEvent_t, may be null) is signalled by the kernel's own completion (hipExtLaunchKernel
 // stop event: no separate marker packet, unlike a hipEventRecord behind the launch).
 int launch_trace(const KParams& p, int prec, void* stream, void* done_event = nullptr);
+// nframes frames of one band in ONE launch (grid.z = frame): d_tab = their KParams in device
+// memory, p0 = a host copy of the first (grid, kernel choice: every frame must share its W,
+// nrows, row_units_log2, depth, flags, precision and scene).  The linear-scan kernels only:
+// hipErrorNotSupported for a wave-cull scene or RT_OPT_PIXEL_PAIRS.
+int launch_trace_batch(const KParams* d_tab, const KParams& p0, int nframes, int prec, void* stream,
+                       void* done_event);
 int max_depth();
 // Device self-test of the exact fp64 helpers against IEEE operations:
 // which 0 = division (shared reciprocal), 1 = integer-exponent pow vs pow(),

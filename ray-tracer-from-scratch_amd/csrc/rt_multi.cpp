@@ -124,6 +124,8 @@ struct Rank {
     hipEvent_t ev_bdone[2] = {};
     // rt_multi_sync: recorded on each render stream and the comm stream, then polled
     hipEvent_t ev_drain[RT_MULTI_SLOTS + 1] = {};
+    // root, RT_OPT_FRAME_BATCH: its rows of a batch rendered (on the batch's first stream)
+    hipEvent_t ev_rows = nullptr;
     // worker thread (local ranks other than the first, one process driving several GPUs)
     std::thread th;
     std::mutex mu;
@@ -212,6 +214,7 @@ struct rt_multi {
     int nranks = 1, nlocal = 1, first_rank = 0, transport = RT_TRANSPORT_RCCL;
     int slots = 2;                  // RT_OPT_MULTI_FRAMES: band slots in use (frames in flight)
     int batch = 1;                  // RT_OPT_MULTI_BATCH: frames per gather
+    int frame_batch = 1;            // RT_OPT_FRAME_BATCH (forwarded to every ctx as well)
     uint64_t nbatch = 0;            // batches gathered (batch slot = nbatch % 2)
     bool fault_next = false;        // RT_OPT_MULTI_FAULT (test hook)
     int layout = 0;                 // RT_OPT_MULTI_LAYOUT: 0 contiguous bands, 1 interleaved,
@@ -990,7 +993,9 @@ int batch_send(rt_multi* m, Rank* k, const BatchJob& b, bool self) {
     // the batch's frames round-robin over RT_OPT_MULTI_FRAMES render streams, so a small
     // band's long last waves overlap the next frames' (one stream would run them one after
     // another), each stream first waiting until this slot's last send is done
-    const int S = std::max(1, std::min(m->slots, b.kb));
+    // (RT_OPT_FRAME_BATCH: every band frame on one stream, so the ctx launches the batch as
+    // one grid — its frames' tails overlap inside the launch)
+    const int S = m->frame_batch > 1 ? 1 : std::max(1, std::min(m->slots, b.kb));
     void* sts[RT_MULTI_SLOTS];
     for (int j = 0; j < S; j++) {
         sts[j] = k->render_stream[j];
@@ -1041,6 +1046,11 @@ int batch_root(rt_multi* m, Rank* k, const BatchJob& b, char* const* frames, hip
     // the next render into that buffer.  The previous batch's buffers wait on its done event;
     // the one before's on ev_bdone[bs], which still holds that batch's record (and the comm
     // stream runs batches in order, so it also covers every older one).
+    // RT_OPT_FRAME_BATCH: the root's rows of every frame of the batch are rendered on the
+    // first frame's stream (one launch); the batch's other caller streams are ordered around it
+    hipStream_t rs[RT_MULTI_BATCH_MAX];
+    for (int i = 0; i < b.kb; i++) rs[i] = m->frame_batch > 1 ? sts[0] : sts[i];
+    const bool one_stream = m->frame_batch > 1 && uniq.size() > 1;
     {
         std::vector<std::pair<hipStream_t, int>> waits;
         const int prev = 1 - b.bs;
@@ -1052,8 +1062,8 @@ int batch_root(rt_multi* m, Rank* k, const BatchJob& b, char* const* frames, hip
             else if (std::find(m->batch_bufs[b.bs].begin(), m->batch_bufs[b.bs].end(), frames[i]) !=
                      m->batch_bufs[b.bs].end())
                 slot = b.bs;
-            if (slot >= 0 && std::find(waits.begin(), waits.end(), std::make_pair(sts[i], slot)) == waits.end())
-                waits.emplace_back(sts[i], slot);
+            if (slot >= 0 && std::find(waits.begin(), waits.end(), std::make_pair(rs[i], slot)) == waits.end())
+                waits.emplace_back(rs[i], slot);
         }
         for (const auto& w : waits) MHIPF(m, hipStreamWaitEvent(w.first, k->ev_bdone[w.second], 0));
     }
@@ -1061,6 +1071,8 @@ int batch_root(rt_multi* m, Rank* k, const BatchJob& b, char* const* frames, hip
     for (size_t u = 0; u < uniq.size(); u++) {
         MHIPF(m, hipEventRecord(m->ev_in[u], uniq[u]));
         MHIPF(m, hipStreamWaitEvent(k->comm_stream, m->ev_in[u], 0));
+        // the root's rows of a frame of stream u, rendered on sts[0], follow u's earlier work
+        if (one_stream && uniq[u] != sts[0]) MHIPF(m, hipStreamWaitEvent(sts[0], m->ev_in[u], 0));
     }
     const Part p0 = part_of(m, cam.height, 0);
     int st = RT_OK;
@@ -1071,12 +1083,18 @@ int batch_root(rt_multi* m, Rank* k, const BatchJob& b, char* const* frames, hip
         void* ss[RT_MULTI_BATCH_MAX];
         for (int i = 0; i < b.kb; i++) {
             outs[i] = frames[i] + (size_t)p0.row0 * row_bytes;
-            ss[i] = sts[i];
+            ss[i] = rs[i];
         }
         SlowCall sc_("rt_render_device_frames (root batch)");
         const int e = rt_render_device_frames(k->ctx, b.cams, b.kb, p0.row0, p0.nrows, b.depth, b.precision,
                                               b.flags, b.out_format, outs, b.kb, ss, b.kb, b.kb);
         st = ctx_err(m, k, e, "rt_render_device_frames (root batch)");
+        if (st == RT_OK && one_stream) {
+            // work the caller enqueues on the batch's other streams sees their frames' rows
+            MHIPF(m, hipEventRecord(k->ev_rows, sts[0]));
+            for (hipStream_t u : uniq)
+                if (u != sts[0]) MHIPF(m, hipStreamWaitEvent(u, k->ev_rows, 0));
+        }
     }
     if (st != RT_OK) return st;
     m->batch_bufs[b.bs].assign(frames, frames + b.kb);
@@ -1212,6 +1230,7 @@ void destroy_rank(Rank* k, bool abort_comm) {
     }
     for (auto e : k->ev_drain)
         if (e) (void)hipEventDestroy(e);
+    if (k->ev_rows) (void)hipEventDestroy(k->ev_rows);
     for (auto& e : k->ev_ready)
         if (e) (void)hipEventDestroy(e);
     for (auto& b : k->staging)
@@ -1565,6 +1584,7 @@ int rt_multi_create(const int32_t* devices, int32_t nlocal, int32_t nranks, int3
         }
         for (auto& ev : k->ev_drain)
             if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&k->ev_rows, hipEventDisableTiming);
         if (e != hipSuccess) fail(hip_err(m, e, "rank streams/events"));
     }
     if (st == RT_OK && m->has_root()) {
@@ -1791,6 +1811,15 @@ int rt_multi_set_option(rt_multi* m, int32_t option, int64_t value) {
     if (option == RT_OPT_MULTI_BATCH) {
         if (value < 1 || value > RT_MULTI_BATCH_MAX) return RT_ERR_INVALID_ARG;
         m->batch = (int)value;  // takes effect from the next rt_multi_render_device_frames
+        return RT_OK;
+    }
+    if (option == RT_OPT_FRAME_BATCH) {
+        if (value < 1 || value > RT_MULTI_BATCH_MAX) return RT_ERR_INVALID_ARG;
+        for (Rank* k : m->r) {
+            const int st = rt_set_option(k->ctx, option, value);
+            if (st != RT_OK) return ctx_err(m, k, st, "rt_set_option");
+        }
+        m->frame_batch = (int)value;  // the batched exchange renders a batch on one stream
         return RT_OK;
     }
     if (option == RT_OPT_MULTI_LAYOUT) {

@@ -818,8 +818,72 @@ __device__ __forceinline__ Wall64 wall64_sload(const Wall64* q) {
                  : "memory");
     return __builtin_bit_cast(Wall64, t);
 }
+/* RT_WALL_PRE32 (A/B): the exact-path scans' walls decided in fp32 first.
+ * Each wall's t and bounds are evaluated in fp32 with wall_cull's error model (relative
+ * error of t <= rel, of the hit point <= err): a wall the exact test must reject (t <= 0 by
+ * the signs, or a point outside the rectangle by more than err) is dropped; a wall it must
+ * accept (signs and bounds clear of the margins) bounds the final best from above by
+ * t (1 + 2 rel); and only the walls whose lower bound t (1 - 2 rel) does not exceed that
+ * bound (or the spheres' best) run the exact fp64 test, in scene order.  Every wall that can
+ * win or tie the final best is among them, so the winner — and h — are bitwise the full
+ * scan's.  fp64 FMAs issue at the fp32 rate on gfx950 (§3), so this pays only if the exact
+ * bodies it skips outweigh the fp32 pass over every wall. */
+#ifndef RT_WALL_PRE32
+#define RT_WALL_PRE32 0
+#endif
+constexpr int PRE32_MAXW = 6;
+template <bool EYE>
+__device__ __forceinline__ void walls_pre32(const KParams& p, const RayD& r, HitD& h) {
+    const RayF rf = make_rayf(r);
+    const float dl = fsqrt(rf.a);
+    float tlo[PRE32_MAXW];
+    double U = h.dist;
+#pragma unroll
+    for (int w = 0; w < PRE32_MAXW; ++w) {
+        tlo[w] = __builtin_nanf("");  // never tested
+        if (w >= p.nW) continue;      // wave-uniform
+        const Wall32& Wl = p.w32[w];
+        const f3 n = F3(Wl.n[0], Wl.n[1], Wl.n[2]), P = F3(Wl.P[0], Wl.P[1], Wl.P[2]);
+        const float den = fdot(n, rf.d);
+        const float num = fdot(P - rf.o, n);
+        const float B = rf.oinf + fmax3abs(P.x, P.y, P.z);
+        const float mnum = CULL_K * B, mden = rf.kb;
+        const bool behind = (num < -mnum && den > mden) || (num > mnum && den < -mden);
+        const bool illc = fabsf(num) <= 64.0f * mnum || fabsf(den) <= 64.0f * mden;
+        const float t = num * frcp(den);
+        // wall_cull's relative error of t, the quotients through reciprocals (+1% for their
+        // own rounding)
+        const float rel = 1.01f * (mnum * frcp(fabsf(num)) + mden * frcp(fabsf(den))) + 4.0f * CULL_U;
+        const f3 q = fmad3(rf.d, t, rf.o) - P;
+        const float len_dt = dl * fabsf(t);
+        const float err = 2.0f * len_dt * rel + CULL_K * (B + len_dt + Wl.len + Wl.wid);
+        const float px = fdot(q, F3(Wl.X[0], Wl.X[1], Wl.X[2]));
+        const float py = fdot(q, F3(Wl.Y[0], Wl.Y[1], Wl.Y[2]));
+        const bool outb = px < -err || px > Wl.len + err || py < -err || py > Wl.wid + err;
+        const bool inb = px >= err && px <= Wl.len - err && py >= err && py <= Wl.wid - err;
+        const float m2 = 2.0f * rel * fabsf(t);
+        const bool never = behind || (!illc && outb);
+        // well conditioned and not behind: fp32 num and den carry the exact signs, so t > 0
+        // here is the exact t > 0
+        const bool sure = !illc && !behind && inb && t > 0.0f;
+        tlo[w] = never ? __builtin_nanf("") : (illc ? -__builtin_inff() : t - m2);
+        if (sure) U = fmin(U, (double)(t + m2));
+    }
+#pragma unroll
+    for (int w = 0; w < PRE32_MAXW; ++w) {
+        if (w >= p.nW) break;
+        if ((double)tlo[w] <= U) wall_exact<EYE>(p.w64[w], w, p, r, h);
+    }
+}
+
 template <bool MIXED, bool EYE = false, bool SL = false>
 __device__ __forceinline__ void walls_d(const KParams& p, const RayD& r, const RayF& rf, HitD& h) {
+    if constexpr (RT_WALL_PRE32 && !MIXED && !SL) {
+        if (p.nW <= PRE32_MAXW) {  // wave-uniform
+            walls_pre32<EYE>(p, r, h);
+            return;
+        }
+    }
     for (int w = 0; w < p.nW; ++w) {
         if (!MIXED && !SL && RT_WALL_PAIRS && w + 1 < p.nW) {
             wall_pair<EYE>(p, w, w + 1, r, h);
@@ -2621,10 +2685,9 @@ __device__ __forceinline__ void trace_tile(const KParams& p, int bx, int trow, i
 }
 
 
+/* One workgroup of a frame's grid (x: tile column or part of one, y: dispatch unit). */
 template <int PREC, bool SUN, bool INT_EXP, bool CULL, int MAXD>
-__global__ void __launch_bounds__(BLOCK)
-__attribute__((amdgpu_waves_per_eu(waves_per_eu<PREC, SUN, INT_EXP, CULL, MAXD>(), 8)))
-k_trace(KParams p) {
+__device__ __forceinline__ void trace_grid(const KParams& p) {
     // workgroup row -> dispatch unit (a tile row, or a part of one: KParams::row_units_log2)
     // the primary pixel boxes (one per lane; wave-start load, used after ray generation)
     const uint64_t braw = (RT_EARLY_LOADS >= 2 && !CULL) ? box_load_primary(p) : 0;
@@ -2672,6 +2735,28 @@ k_trace(KParams p) {
     trace_tile<PREC, SUN, INT_EXP, CULL, MAXD>(p, bx, u >> ul, gx, braw);
 #endif
 }
+
+template <int PREC, bool SUN, bool INT_EXP, bool CULL, int MAXD>
+__global__ void __launch_bounds__(BLOCK)
+__attribute__((amdgpu_waves_per_eu(waves_per_eu<PREC, SUN, INT_EXP, CULL, MAXD>(), 8)))
+k_trace(KParams p) {
+    trace_grid<PREC, SUN, INT_EXP, CULL, MAXD>(p);
+}
+
+#if !RT_STAMP
+/* A batch of frames of one band in ONE launch (rt_render_device_frames with
+ * RT_OPT_FRAME_BATCH): frame blockIdx.z's kernel arguments come from a device table the host
+ * filled (one KParams per frame, copied in behind the previous work on the stream), the
+ * same code as k_trace otherwise.  The table is read-only and not aliased by anything the
+ * kernel writes, so its fields load through the scalar path like kernel arguments.  The
+ * linear-scan kernels only (the cull kernels' frames take one launch each). */
+template <int PREC, bool SUN, bool INT_EXP, int MAXD>
+__global__ void __launch_bounds__(BLOCK)
+__attribute__((amdgpu_waves_per_eu(waves_per_eu<PREC, SUN, INT_EXP, false, MAXD>(), 8)))
+k_trace_tab(const KParams* __restrict__ tab) {
+    trace_grid<PREC, SUN, INT_EXP, false, MAXD>(tab[blockIdx.z]);
+}
+#endif
 
 /* PATH64 linear scan, two pixels per lane (trace_pair_p64): tile pair bp of dispatch unit
  * u covers tile columns 2bp and 2bp + 1 of its tile row. */
@@ -2729,7 +2814,17 @@ static hipError_t launch_pair(const KParams& p, dim3 grid, hipStream_t st, hipEv
 #endif  // RT_WAVES_PER_BLOCK == 1 && !RT_TILE_PAIRS
 
 template <int PREC, bool SUN, bool INT_EXP, bool CULL, int MAXD>
-static void launch_one(const KParams& p, dim3 grid, hipStream_t st, hipEvent_t done) {
+static void launch_one(const KParams& p, dim3 grid, hipStream_t st, hipEvent_t done,
+                       const KParams* tab) {
+#if !RT_STAMP
+    if constexpr (!CULL) {
+        if (tab) {  // grid.z frames, their arguments in the device table
+            hipExtLaunchKernelGGL((k_trace_tab<PREC, SUN, INT_EXP, MAXD>), grid, dim3(BLOCK), 0, st,
+                                  nullptr, done, 0, tab);
+            return;
+        }
+    }
+#endif
     if (done)
         hipExtLaunchKernelGGL((k_trace<PREC, SUN, INT_EXP, CULL, MAXD>), grid, dim3(BLOCK), 0, st,
                               nullptr, done, 0, p);
@@ -2737,45 +2832,49 @@ static void launch_one(const KParams& p, dim3 grid, hipStream_t st, hipEvent_t d
         hipLaunchKernelGGL((k_trace<PREC, SUN, INT_EXP, CULL, MAXD>), grid, dim3(BLOCK), 0, st, p);
 }
 template <int PREC, bool SUN, bool INT_EXP, bool CULL>
-static hipError_t launch_depth(const KParams& p, dim3 grid, hipStream_t st, hipEvent_t done) {
+static hipError_t launch_depth(const KParams& p, dim3 grid, hipStream_t st, hipEvent_t done,
+                               const KParams* tab) {
     if constexpr (RT_AB_SLIM && (PREC != PREC_PATH64 || SUN)) {
         return hipErrorInvalidValue;
     } else if constexpr (RT_AB_SLIM) {
         if (p.depth <= MAXD_SMALL)
-            launch_one<PREC, SUN, INT_EXP, CULL, MAXD_SMALL>(p, grid, st, done);
+            launch_one<PREC, SUN, INT_EXP, CULL, MAXD_SMALL>(p, grid, st, done, tab);
         else if (p.depth <= MAXD_MID)
-            launch_one<PREC, SUN, INT_EXP, CULL, MAXD_MID>(p, grid, st, done);
+            launch_one<PREC, SUN, INT_EXP, CULL, MAXD_MID>(p, grid, st, done, tab);
         else
             return hipErrorInvalidValue;
         return hipGetLastError();
     } else {
         if (p.depth <= MAXD_SMALL)
-            launch_one<PREC, SUN, INT_EXP, CULL, MAXD_SMALL>(p, grid, st, done);
+            launch_one<PREC, SUN, INT_EXP, CULL, MAXD_SMALL>(p, grid, st, done, tab);
         else if (p.depth <= MAXD_MID)
-            launch_one<PREC, SUN, INT_EXP, CULL, MAXD_MID>(p, grid, st, done);
+            launch_one<PREC, SUN, INT_EXP, CULL, MAXD_MID>(p, grid, st, done, tab);
         else if (p.depth <= MAXD_REF)
-            launch_one<PREC, SUN, INT_EXP, CULL, MAXD_REF>(p, grid, st, done);
+            launch_one<PREC, SUN, INT_EXP, CULL, MAXD_REF>(p, grid, st, done, tab);
         else
-            launch_one<PREC, SUN, INT_EXP, CULL, MAXD_LARGE>(p, grid, st, done);
+            launch_one<PREC, SUN, INT_EXP, CULL, MAXD_LARGE>(p, grid, st, done, tab);
         return hipGetLastError();
     }
 }
 template <int PREC, bool SUN, bool INT_EXP>
-static hipError_t launch_cull(const KParams& p, dim3 grid, hipStream_t st, hipEvent_t done) {
-    return p.wave_cull ? launch_depth<PREC, SUN, INT_EXP, true>(p, grid, st, done)
-                       : launch_depth<PREC, SUN, INT_EXP, false>(p, grid, st, done);
+static hipError_t launch_cull(const KParams& p, dim3 grid, hipStream_t st, hipEvent_t done,
+                              const KParams* tab) {
+    if (tab && p.wave_cull) return hipErrorNotSupported;  // no table kernels for the cull path
+    return p.wave_cull ? launch_depth<PREC, SUN, INT_EXP, true>(p, grid, st, done, tab)
+                       : launch_depth<PREC, SUN, INT_EXP, false>(p, grid, st, done, tab);
 }
 template <int PREC>
-static hipError_t launch_prec(const KParams& p, dim3 grid, hipStream_t st, hipEvent_t done) {
+static hipError_t launch_prec(const KParams& p, dim3 grid, hipStream_t st, hipEvent_t done,
+                              const KParams* tab = nullptr) {
     if constexpr (PREC == PREC_F64 || PREC == PREC_MIXED) {
         if (p.flags & FLAG_SUN)
-            return p.int_exp ? launch_cull<PREC, true, true>(p, grid, st, done)
-                             : launch_cull<PREC, true, false>(p, grid, st, done);
-        return p.int_exp ? launch_cull<PREC, false, true>(p, grid, st, done)
-                         : launch_cull<PREC, false, false>(p, grid, st, done);
+            return p.int_exp ? launch_cull<PREC, true, true>(p, grid, st, done, tab)
+                             : launch_cull<PREC, true, false>(p, grid, st, done, tab);
+        return p.int_exp ? launch_cull<PREC, false, true>(p, grid, st, done, tab)
+                         : launch_cull<PREC, false, false>(p, grid, st, done, tab);
     } else {
-        return (p.flags & FLAG_SUN) ? launch_cull<PREC, true, true>(p, grid, st, done)
-                                    : launch_cull<PREC, false, true>(p, grid, st, done);
+        return (p.flags & FLAG_SUN) ? launch_cull<PREC, true, true>(p, grid, st, done, tab)
+                                    : launch_cull<PREC, false, true>(p, grid, st, done, tab);
     }
 }
 
@@ -2790,14 +2889,25 @@ extern "C" int rt_diag_read(unsigned long long* out16) {
 }
 #endif
 
-int launch_trace_ns(const KParams& p, int prec, void* stream, void* done_event) {
+int launch_trace_ns(const KParams& p, int prec, void* stream, void* done_event,
+                    const KParams* d_tab = nullptr, int nframes = 1) {
     if (p.W <= 0 || p.nrows <= 0) return (int)hipSuccess;
     const int ul = p.row_units_log2;
     const int units = ((p.nrows + TILE_H - 1) / TILE_H) << ul;
     const dim3 grid((((p.W + TILE_W - 1) / TILE_W) + (1 << ul) - 1) >> ul,
-                    RT_TILE_PAIRS ? (units + 1) / 2 : units);
+                    RT_TILE_PAIRS ? (units + 1) / 2 : units, d_tab ? nframes : 1);
     hipStream_t st = static_cast<hipStream_t>(stream);
     hipEvent_t done = static_cast<hipEvent_t>(done_event);
+    if (d_tab) {  // a batch of frames: the table kernels (linear scan, one pixel per lane)
+        if (RT_TILE_PAIRS || p.wave_cull || p.pairs) return (int)hipErrorNotSupported;
+        switch (prec) {
+            case PREC_F64: return (int)launch_prec<PREC_F64>(p, grid, st, done, d_tab);
+            case PREC_F32: return (int)launch_prec<PREC_F32>(p, grid, st, done, d_tab);
+            case PREC_MIXED: return (int)launch_prec<PREC_MIXED>(p, grid, st, done, d_tab);
+            case PREC_PATH64: return (int)launch_prec<PREC_PATH64>(p, grid, st, done, d_tab);
+            default: return (int)hipErrorInvalidValue;
+        }
+    }
     // two pixels per lane exist only in one-wave (8x8 tile) builds: the pair kernel is not
     // instantiated for RT_WAVES_PER_BLOCK > 1 or RT_TILE_PAIRS (RT_OPT_PIXEL_PAIRS ignored)
 #if RT_WAVES_PER_BLOCK == 1 && !RT_TILE_PAIRS && !RT_AB_SLIM
@@ -2925,6 +3035,11 @@ int launch_trace(const KParams& p, int prec, void* stream, void* done_event) {
                                   : kno::launch_trace_ns(p, prec, stream, done_event);
 }
 int max_depth() { return kno::max_depth_ns(); }
+int launch_trace_batch(const KParams* d_tab, const KParams& p0, int nframes, int prec, void* stream,
+                       void* done_event) {
+    if (nframes <= 0) return (int)hipSuccess;
+    return kno::launch_trace_ns(p0, prec, stream, done_event, d_tab, nframes);
+}
 int launch_selftest(int which, uint64_t n, uint64_t seed, unsigned long long* d_bad,
                     void* stream) {
     return kno::launch_selftest_ns(which, n, seed, d_bad, stream);

@@ -73,6 +73,7 @@ RT_OPT_MULTI_FRAMES = 17
 RT_OPT_MULTI_FAULT = 18
 RT_OPT_MULTI_BATCH = 19
 RT_OPT_MULTI_TIMEOUT_MS = 20
+RT_OPT_FRAME_BATCH = 21
 RT_OPT_ROW_FEEDBACK_EMA = 14
 RT_OPT_ROW_FEEDBACK_ISOLATE = 15
 

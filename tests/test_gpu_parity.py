@@ -877,6 +877,56 @@ def test_render_device_frames_equals_per_frame_calls(rend):
     rend.set_option(capi.RT_OPT_HOST_PIPELINE, 1)
 
 
+@pytest.mark.parametrize("prec", [capi.RT_PREC_PATH64, capi.RT_PREC_F64, capi.RT_PREC_F32])
+def test_frame_batch_launches_equal_per_frame_launches(rend, prec):
+    """RT_OPT_FRAME_BATCH (one launch per batch of band frames): consecutive
+    frames on one stream go to the GPU as one grid (frame = blockIdx.z, arguments from a
+    device table).  A moving camera, 13 frames — into 13 distinct buffers (groups of B = 4,
+    the last one short), into 5 buffers (a group breaks at a repeated buffer, in order), and
+    over 2 alternating streams (groups of one) — every buffer bitwise equal to the per-frame
+    render of its last camera; with the row feedback sampling every second frame (sampled
+    frames leave the group and launch alone through the stamped kernels) and off; a full
+    frame and a ragged band; the c2 scene in the bench precision and the others."""
+    import torch
+    dev = torch.device("cuda", 0)
+    sc = scenes.CONFIGS["c2"].scene()
+    rend.set_scene(scenes.to_prims(sc))
+    W, H = 320, 180
+    ca = scenes.camera_args(W, H)
+    cams = []
+    for k in range(6):
+        a = dict(ca)
+        a["position"] = (ca["position"][0] + 0.04 * k, ca["position"][1], ca["position"][2])
+        cams.append(capi.camera_init(**a))
+    fmt = capi.RT_OUT_RGB_F32
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    nf = 13
+    try:
+        for r0, n in ((0, H), (21, 97)):
+            rend.set_option(capi.RT_OPT_FRAME_BATCH, 1)
+            refs = [rend.render(c, 4, prec, 0, fmt, row0=r0, nrows=n)[0] for c in cams]
+            for fb_rows in (2, 0):
+                rend.set_option(capi.RT_OPT_ROW_FEEDBACK, fb_rows)
+                rend.set_option(capi.RT_OPT_FRAME_BATCH, 4)
+                for nb, sts in ((13, [s1]), (5, [s1]), (4, [s1, s2])):
+                    outs = [torch.full((n, W, 3), -1.0, device=dev) for _ in range(nb)]
+                    torch.cuda.synchronize()
+                    rend.render_device_frames(cams, 4, [o.data_ptr() for o in outs], prec, 0, fmt,
+                                              row0=r0, nrows=n, streams=[s.cuda_stream for s in sts],
+                                              nframes=nf)
+                    torch.cuda.synchronize()
+                    for b, o in enumerate(outs):
+                        lf = max(f for f in range(nf) if f % nb == b)
+                        assert np.array_equal(o.cpu().numpy().view(np.uint32),
+                                              refs[lf % len(cams)].view(np.uint32)), (r0, fb_rows, nb, b)
+        for bad in (0, capi.RT_MULTI_BATCH_MAX + 1):
+            with pytest.raises(capi.RTError):
+                rend.set_option(capi.RT_OPT_FRAME_BATCH, bad)
+    finally:
+        rend.set_option(capi.RT_OPT_FRAME_BATCH, 1)
+        rend.set_option(capi.RT_OPT_ROW_FEEDBACK, 32)
+
+
 def test_row_feedback_isolated_sampling_in_flight(rend):
     """Row feedback on frames in flight (three caller streams, a snapshot every other
     frame): with RT_OPT_ROW_FEEDBACK_ISOLATE on (default off) the sampled frames are ordered

@@ -411,15 +411,18 @@ def test_batched_gather_ragged_empty_bands_and_root_limits(rend, W, fmt):
             assert np.array_equal(b.cpu().numpy().view(np.uint32), refs[0].view(np.uint32))
 
 
-@pytest.mark.parametrize("transport", ["threads", "loopback"])
-def test_batched_frames_each_whole_in_its_own_buffer(rend, transport):
+@pytest.mark.parametrize("transport,frame_batch", [("threads", 1), ("loopback", 1), ("threads", 4),
+                                                   ("loopback", 4)])
+def test_batched_frames_each_whole_in_its_own_buffer(rend, transport, frame_batch):
     """B = 4 frames of a moving camera into 4 distinct buffers — every buffer
     bitwise against ITS OWN one-GPU frame (not only the last frame written) — then 4 more
     frames into the same 4 buffers (a batch revisiting an earlier batch's buffers), again
     every buffer.  Over 3 THREADS handles (the process-per-GPU shape) and the one-rank
     loopback RCCL communicator.  Then the refusal: 4 frames over 2 buffers is RT_ERR_UNSUPPORTED
     on the root before anything is enqueued; the one-rank handle stays usable, and with
-    peers (THREADS) the exchange ends for every handle (RT_ERR_COMM, no hang)."""
+    peers (THREADS) the exchange ends for every handle (RT_ERR_COMM, no hang).
+    frame_batch 4 (RT_OPT_FRAME_BATCH): every rank's band frames of a batch, and the root's
+    rows of them over its two caller streams, go to the GPU as one launch."""
     import os
     import torch
     dev = torch.device("cuda", 0)
@@ -443,6 +446,7 @@ def test_batched_frames_each_whole_in_its_own_buffer(rend, transport):
         for h in hs:
             h.set_scene(prims)
             h.set_option(capi.RT_OPT_MULTI_BATCH, 4)
+            h.set_option(capi.RT_OPT_FRAME_BATCH, frame_batch)
         torch.cuda.synchronize()
 
         def call(cs, ptrs):

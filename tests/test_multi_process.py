@@ -1,7 +1,8 @@
 """The multi-GPU frame operator's process-per-GPU path in REAL separate processes on one
 MI355X: RT_TRANSPORT_IPC (include/rt_capi.h) — one process per rank, each an rt_multi handle
-(nlocal = 1, first_rank = its rank), the exchange through a shared-memory mailbox with the
-root's staging buffers and every rank's exchange events shared by HIP IPC.  Everything
+(nlocal = 1, first_rank = its rank), the exchange through a shared-memory mailbox, the
+root's staging buffers shared by HIP IPC, the stream order across processes kept by
+shared-memory counters set and awaited on the streams (host functions).  Everything
 around the copies is the RCCL path's code (band slots, the batched exchange, the root's
 staging and scatter, the non-root caller-stream waits, failure handling).
 
@@ -41,6 +42,7 @@ def _worker(rank, n, uid, case, q):
         dev = torch.device("cuda", 0)
         w, h, nf, layout, batch, slots, weights, fault = (case[k] for k in (
             "w", "h", "nf", "layout", "batch", "slots", "weights", "fault"))
+        fbatch = case.get("frame_batch", 1)
         prims = scenes.to_prims(scenes.CONFIGS["c2"].scene())
         cams = [_cam(w, h, 0.02 * k) for k in range(5)]
         m = capi.MultiRenderer([0], nranks=n, first_rank=rank, unique_id=uid,
@@ -50,6 +52,7 @@ def _worker(rank, n, uid, case, q):
             m.set_option(capi.RT_OPT_MULTI_LAYOUT, layout)
             m.set_option(capi.RT_OPT_MULTI_FRAMES, slots)
             m.set_option(capi.RT_OPT_MULTI_BATCH, batch)
+            m.set_option(capi.RT_OPT_FRAME_BATCH, fbatch)
             m.set_option(capi.RT_OPT_MULTI_TIMEOUT_MS, 60000)
             if weights is not None:
                 m.set_row_weights(weights)
@@ -104,14 +107,15 @@ def rend():
     r.close()
 
 
-@pytest.mark.parametrize("n,w,h,layout,batch,slots", [
-    (2, 1920, 1080, 0, 1, 2),    # config 4's frame, per-frame exchange, contiguous bands
-    (2, 1920, 1080, 0, 4, 4),    # config 4's frame, the batched exchange bench.py times
-    (3, 480, 270, 1, 1, 2),      # interleaved parts (staging + strided scatter)
-    (4, 640, 360, 2, 3, 3),      # cost-weighted bands, batched (a third batch revisits buffers)
-    (4, 203, 117, 0, 2, 2),      # ragged bands, 1-byte-misaligned rows
+@pytest.mark.parametrize("n,w,h,layout,batch,slots,fbatch", [
+    (2, 1920, 1080, 0, 1, 2, 1),    # config 4's frame, per-frame exchange, contiguous bands
+    (2, 1920, 1080, 2, 4, 4, 4),    # config 4's frame, the batched exchange bench.py times
+    (3, 480, 270, 1, 1, 2, 1),      # interleaved parts (staging + strided scatter)
+    (4, 640, 360, 2, 3, 3, 1),      # cost-weighted bands, batched (a third batch revisits buffers)
+    (4, 640, 360, 0, 3, 3, 3),      # the same with one launch per batch (RT_OPT_FRAME_BATCH)
+    (4, 203, 117, 0, 2, 2, 1),      # ragged bands, 1-byte-misaligned rows
 ])
-def test_ipc_processes_gather_bitwise(rend, n, w, h, layout, batch, slots):
+def test_ipc_processes_gather_bitwise(rend, n, w, h, layout, batch, slots, fbatch):
     from rtamd import capi, scenes
     prims = scenes.to_prims(scenes.CONFIGS["c2"].scene())
     rend.set_scene(prims)
@@ -121,7 +125,7 @@ def test_ipc_processes_gather_bitwise(rend, n, w, h, layout, batch, slots):
     nf = 7
     nb = 2 if batch == 1 else min(nf, 2 * batch)
     case = dict(w=w, h=h, nf=nf, layout=layout, batch=batch, slots=slots, weights=weights,
-                fault=0, nb=nb)
+                fault=0, nb=nb, frame_batch=fbatch)
     res = _run(n, case)
     assert all(r["status"] == 0 for r in res), [(r["rank"], r["status"], r["error"]) for r in res]
     bufs = res[0]["bufs"]

@@ -12,9 +12,11 @@ GPU with the GPU held busy behind a spin kernel (so no call waits for it):
     hipEventRecord(ev_sent[s], comm)
     hipStreamWaitEvent(caller, ev_sent[s])           only when the caller passes a stream
 
-Also each piece alone, the render through the pipelined frame loop, and the RCCL one-rank
-loopback operator's frame (its root enqueues a self ncclSend/ncclRecv group per frame, or per
-batch of 4 or 10 frames with RT_OPT_MULTI_BATCH).
+Also each piece alone, the render through the pipelined frame loop (per-frame launches, and
+RT_OPT_FRAME_BATCH = 4 / 8: a rank's band frames on one stream as one launch per group), and
+the RCCL one-rank loopback operator's frame (its root enqueues a self ncclSend/ncclRecv group
+per frame, or per batch of 4 or 10 frames with RT_OPT_MULTI_BATCH, with and without
+RT_OPT_FRAME_BATCH; 2 B frame buffers, as a batch needs a distinct buffer per frame).
 One GPU, one process: the runtime serialises nothing here that a rank process would not.
 
     python tools/nonroot_host_cost.py > nonroot.json   (CFG=c2, NB=8 by default)
@@ -46,7 +48,7 @@ def main():
     rs = [torch.cuda.Stream(dev) for _ in range(slots)]
     comm = torch.cuda.Stream(dev)
     caller = torch.cuda.Stream(dev)
-    band = [torch.empty(nbytes, dtype=torch.uint8, device=dev) for _ in range(slots)]
+    band = [torch.empty(nbytes, dtype=torch.uint8, device=dev) for _ in range(16)]
     dst = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     hip = C.CDLL("libamdhip64.so")
     hip.hipEventCreateWithFlags.argtypes = [C.POINTER(C.c_void_p), C.c_uint]
@@ -103,8 +105,16 @@ def main():
            "frames_per_call": n}
     res["render_only"] = timed(lambda: [render(f % slots) for f in range(n)])
     res["render_frames_pipelined"] = timed(lambda: r.render_device_frames(
-        [cam], cfg.depth, [b.data_ptr() for b in band], capi.RT_PREC_PATH64, 0, fmt, row0=r0,
+        [cam], cfg.depth, [b.data_ptr() for b in band[:slots]], capi.RT_PREC_PATH64, 0, fmt, row0=r0,
         nrows=nr, streams=[s_.cuda_stream for s_ in rs], nframes=n))
+    # a batch's band frames on ONE stream (what rt_multi's batch_send does with
+    # RT_OPT_FRAME_BATCH): per-frame launches vs one launch per group of B
+    for fb in (1, 4, 8):
+        r.set_option(capi.RT_OPT_FRAME_BATCH, fb)
+        res[f"render_frames_one_stream_frame_batch{fb}"] = timed(lambda: r.render_device_frames(
+            [cam], cfg.depth, [b.data_ptr() for b in band[:max(fb, 4)]], capi.RT_PREC_PATH64, 0, fmt,
+            row0=r0, nrows=nr, streams=[rs[0].cuda_stream], nframes=n))
+    r.set_option(capi.RT_OPT_FRAME_BATCH, 1)
     res["hipEventRecord"] = timed(lambda: [hip.hipEventRecord(ev_rendered[f % slots], C.c_void_p(
         rs[f % slots].cuda_stream)) for f in range(n)])
     res["hipStreamWaitEvent"] = timed(lambda: [hip.hipStreamWaitEvent(C.c_void_p(comm.cuda_stream),
@@ -117,14 +127,17 @@ def main():
     res["nonroot_frame_copy_send_caller_wait"] = timed(lambda: [frame(f, True, True) for f in range(n)])
     r.close()
     # the one-rank operators: COPY (no exchange) and RCCL loopback (a self send/recv group)
-    for name, tr, b in (("multi_1_copy", capi.RT_TRANSPORT_COPY, 1),
-                        ("multi_1_loopback", capi.RT_TRANSPORT_RCCL_LOOPBACK, 1),
-                        ("multi_1_loopback_batch4", capi.RT_TRANSPORT_RCCL_LOOPBACK, 4),
-                        ("multi_1_loopback_batch10", capi.RT_TRANSPORT_RCCL_LOOPBACK, 10)):
-        frames = [torch.empty(H * W * 4, dtype=torch.uint8, device=dev) for _ in range(2)]
+    for name, tr, b, fb in (("multi_1_copy", capi.RT_TRANSPORT_COPY, 1, 1),
+                            ("multi_1_loopback", capi.RT_TRANSPORT_RCCL_LOOPBACK, 1, 1),
+                            ("multi_1_loopback_batch4", capi.RT_TRANSPORT_RCCL_LOOPBACK, 4, 1),
+                            ("multi_1_loopback_batch4_frame_batch", capi.RT_TRANSPORT_RCCL_LOOPBACK, 4, 4),
+                            ("multi_1_loopback_batch8_frame_batch", capi.RT_TRANSPORT_RCCL_LOOPBACK, 8, 8),
+                            ("multi_1_loopback_batch10", capi.RT_TRANSPORT_RCCL_LOOPBACK, 10, 1)):
+        frames = [torch.empty(H * W * 4, dtype=torch.uint8, device=dev) for _ in range(max(2, 2 * b))]
         with capi.MultiRenderer([0], transport=tr) as m:
             m.set_scene(prims)
             m.set_option(capi.RT_OPT_MULTI_BATCH, b)
+            m.set_option(capi.RT_OPT_FRAME_BATCH, fb)
             sp = [rs[0].cuda_stream, rs[1].cuda_stream]
             m.render_device_frames([cam], cfg.depth, [f_.data_ptr() for f_ in frames], capi.RT_PREC_PATH64,
                                    0, fmt, streams=sp, nframes=4)
