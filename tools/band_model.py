@@ -7,6 +7,10 @@ and the bytes it sends to the root.  The gather term needs the xGMI link rate, w
 GPU cannot measure: the model takes it as a parameter.
 With --layout interleaved the parts are rt_interleaved_rows parts (tile rows dealt
 round-robin, rt_render_device_interleaved), launched one at a time behind a GPU spin.
+With --frame-batch B (contiguous / weighted bands) each band is also measured the way a rank
+runs it under RT_OPT_FRAME_BATCH: its frames on ONE stream into B distinct buffers, B frames
+per launch — GPU time per frame (kernel_us_fbB) and host time per frame behind a GPU spin
+(host_us_fbB).
     python tools/band_model.py [--config c2] [--precision path64] [--layout contiguous]"""
 import argparse
 import json
@@ -91,6 +95,8 @@ def main():
     ap.add_argument("--precision", default="path64")
     ap.add_argument("--launches", type=int, default=100)
     ap.add_argument("--splits", default="1,2,4,8")
+    ap.add_argument("--frame-batch", type=int, default=0,
+                    help="also time B frames per launch (RT_OPT_FRAME_BATCH) on one stream")
     ap.add_argument("--layout", choices=("contiguous", "interleaved", "weighted"), default="contiguous",
                     help="weighted: contiguous bands cut by rt_weighted_band_rows over the "
                          "measured tile-row costs of one full-frame render (rt_tile_row_costs)")
@@ -159,9 +165,33 @@ def main():
                 streams=[x.cuda_stream for x in sts_], nframes=m)
             fif2 = pipelined_us(torch, st, st2, lo, n, frames=fr)
             fif4 = pipelined_us(torch, st, st2, lo, n, extra, frames=fr)
+            fbk = {}
+            if args.frame_batch > 1:
+                B = args.frame_batch
+                rend.set_option(capi.RT_OPT_FRAME_BATCH, B)
+                bufs = [out, out2] + [torch.empty((nr, W, 3), device=dev) for _ in range(B - 2)]
+                ptrs = [b_.data_ptr() for b_ in bufs[:B]]
+                for timed in (False, True):
+                    torch.cuda.synchronize()
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(st)
+                    rend.render_device_frames([cam], cfg.depth, ptrs, prec, row0=r0, nrows=nr,
+                                              streams=[st.cuda_stream], nframes=n if timed else 2 * B)
+                    e1.record(st)
+                    torch.cuda.synchronize()
+                fbk[f"kernel_us_fb{B}"] = round(e0.elapsed_time(e1) / n * 1e3, 2)
+                with torch.cuda.stream(st):
+                    torch.cuda._sleep(int(2e8))
+                t0 = time.perf_counter()
+                rend.render_device_frames([cam], cfg.depth, ptrs, prec, row0=r0, nrows=nr,
+                                          streams=[st.cuda_stream], nframes=n)
+                fbk[f"host_us_fb{B}"] = round((time.perf_counter() - t0) / n * 1e6, 2)
+                torch.cuda.synchronize()
+                rend.set_option(capi.RT_OPT_FRAME_BATCH, 1)
+                del bufs
             rend.close()
             bands.append({"rank": r, "row0": r0, "nrows": nr, "kernel_us": round(kms * 1e3, 2),
-                          "kernel_us_fif2": fif2, "kernel_us_fif4": fif4,
+                          "kernel_us_fif2": fif2, "kernel_us_fif4": fif4, **fbk,
                           "host_us": round(host_us, 2), "segments": int(segs.item()),
                           "send_bytes_f32": 0 if r == 0 else nr * W * 12,
                           "send_bytes_rgba8": 0 if r == 0 else nr * W * 4})
@@ -171,6 +201,9 @@ def main():
             "max_kernel_us_fif2": max(b["kernel_us_fif2"] for b in bands),
             "max_kernel_us_fif4": max(b["kernel_us_fif4"] for b in bands),
             "max_host_us": max(b["host_us"] for b in bands),
+            **({f"max_kernel_us_fb{args.frame_batch}": max(b[f"kernel_us_fb{args.frame_batch}"] for b in bands),
+                f"max_host_us_fb{args.frame_batch}": max(b[f"host_us_fb{args.frame_batch}"] for b in bands)}
+               if args.frame_batch > 1 and not inter else {}),
             "root_in_bytes_f32": sum(b["send_bytes_f32"] for b in bands),
             "root_in_bytes_rgba8": sum(b["send_bytes_rgba8"] for b in bands),
             "max_link_bytes_f32": max(b["send_bytes_f32"] for b in bands),
