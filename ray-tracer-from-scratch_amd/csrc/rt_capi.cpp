@@ -183,7 +183,7 @@ struct rt_ctx {
     // launch.  TAB_SLOTS groups may be in flight; a slot is reused once its launch (whose
     // stop event is tab_ev[slot]) has completed.
     int frame_batch = 1;
-    static constexpr int TAB_SLOTS = 16;
+    static constexpr int TAB_SLOTS = 64;
     rt::KParams* h_tab = nullptr;  // pinned, TAB_SLOTS x RT_MULTI_BATCH_MAX
     rt::KParams* d_tab = nullptr;  // device, the same
     hipEvent_t tab_ev[TAB_SLOTS] = {};

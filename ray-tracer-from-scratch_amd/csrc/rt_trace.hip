@@ -2747,14 +2747,19 @@ k_trace(KParams p) {
 /* A batch of frames of one band in ONE launch (rt_render_device_frames with
  * RT_OPT_FRAME_BATCH): frame blockIdx.z's kernel arguments come from a device table the host
  * filled (one KParams per frame, copied in behind the previous work on the stream), the
- * same code as k_trace otherwise.  The table is read-only and not aliased by anything the
- * kernel writes, so its fields load through the scalar path like kernel arguments.  The
- * linear-scan kernels only (the cull kernels' frames take one launch each). */
+ * same code as k_trace otherwise.  The table is addressed in the constant address space
+ * (it is read-only while the kernel runs), like the kernel-argument segment: its fields
+ * load through the scalar path and the pointers in it are known global — through a plain
+ * pointer the compiler could not prove the table unclobbered by the kernel's own stores and
+ * turned every access into a per-lane flat load.  The linear-scan kernels only (the cull
+ * kernels' frames take one launch each). */
+typedef __attribute__((address_space(4))) const KParams ConstKParams;
 template <int PREC, bool SUN, bool INT_EXP, int MAXD>
 __global__ void __launch_bounds__(BLOCK)
 __attribute__((amdgpu_waves_per_eu(waves_per_eu<PREC, SUN, INT_EXP, false, MAXD>(), 8)))
-k_trace_tab(const KParams* __restrict__ tab) {
-    trace_grid<PREC, SUN, INT_EXP, false, MAXD>(tab[blockIdx.z]);
+k_trace_tab(uint64_t tab_addr) {
+    ConstKParams* tab = (ConstKParams*)tab_addr;
+    trace_grid<PREC, SUN, INT_EXP, false, MAXD>(*(const KParams*)&tab[blockIdx.z]);
 }
 #endif
 
@@ -2820,7 +2825,7 @@ static void launch_one(const KParams& p, dim3 grid, hipStream_t st, hipEvent_t d
     if constexpr (!CULL) {
         if (tab) {  // grid.z frames, their arguments in the device table
             hipExtLaunchKernelGGL((k_trace_tab<PREC, SUN, INT_EXP, MAXD>), grid, dim3(BLOCK), 0, st,
-                                  nullptr, done, 0, tab);
+                                  nullptr, done, 0, (uint64_t)(uintptr_t)tab);
             return;
         }
     }
