@@ -277,7 +277,8 @@ def main(argv=None) -> int:
                          "kernel (the per-frame exchange's host calls cost more than a 1/8 band)")
     ap.add_argument("--frame-batch", type=int, default=0,
                     help="RT_OPT_FRAME_BATCH: a rank's band frames of one gather go to the GPU as "
-                         "one launch (0 = auto: the gather's batch at N > 1, else 1)")
+                         "one launch (0 = auto: the gather's batch at N > 1, else 1); at N = 1 an "
+                         "explicit B > 1 launches B consecutive frames of a stream as one grid")
     ap.add_argument("--local-ranks", type=int, default=1,
                     help="rehearsal only (one process): split the frame over this many ranks "
                          "on this one GPU with the peer-copy transport; not a measurement")
@@ -365,6 +366,8 @@ def main(argv=None) -> int:
     PHASE[0] = "setup"
 
     rend = capi.Renderer(local)   # census, side measurements, frames mode, kernel time
+    if world == 1 and args.frame_batch > 1:
+        rend.set_option(capi.RT_OPT_FRAME_BATCH, min(capi.RT_MULTI_BATCH_MAX, args.frame_batch))
     rend.set_option(capi.RT_OPT_BOX_CACHE, args.box_cache)
     rend.set_option(capi.RT_OPT_ROW_FEEDBACK, args.row_feedback)
     rend.set_scene(prims)
@@ -413,6 +416,9 @@ def main(argv=None) -> int:
     nbuf = fif
     if tiled_mode and tiler == "native" and (world > 1 or args.local_ranks > 1) and full:
         nbuf = max(fif, 2 * rank_batch)
+    fb1 = world == 1 and args.local_ranks <= 1 and args.frame_batch > 1   # N = 1 frame batching
+    if fb1:
+        nbuf = max(nbuf, args.frame_batch)
     outs = [torch.empty((H if full else max(1, nrows), W, 3), dtype=torch.float32, device=dev)
             for _ in range(nbuf)]
     out = outs[0]
@@ -454,6 +460,8 @@ def main(argv=None) -> int:
         multi.set_option(capi.RT_OPT_BOX_CACHE, args.box_cache)
         multi.set_option(capi.RT_OPT_ROW_FEEDBACK, args.row_feedback)
         multi.set_option(capi.RT_OPT_MULTI_TIMEOUT_MS, int(args.deadline * 1000))
+        if fb1:   # N = 1: the one band is the frame, rendered by the operator's own ctx
+            multi.set_option(capi.RT_OPT_FRAME_BATCH, min(capi.RT_MULTI_BATCH_MAX, args.frame_batch))
         multi.set_scene(prims)
         if layout == 2:
             multi.set_row_weights(weights)
@@ -975,7 +983,8 @@ def main(argv=None) -> int:
                 "band_layout": args.band_layout if (tiled_mode and (world > 1 or args.local_ranks > 1)) else None,
                 "rank_frames_in_flight": args.rank_frames if (tiled_mode and (world > 1 or args.local_ranks > 1)) else None,
                 "frames_per_gather": args.rank_batch if (tiled_mode and world > 1) else None,
-                "frames_per_launch": frame_batch if (multi is not None and multi.nranks > 1) else 1,
+                "frames_per_launch": (frame_batch if (multi is not None and multi.nranks > 1)
+                                      else (args.frame_batch if fb1 else 1)),
                 "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
                 "host_box_cache": bool(args.box_cache),
                 "row_feedback": args.row_feedback,
