@@ -96,7 +96,10 @@ def main():
     ap.add_argument("--launches", type=int, default=100)
     ap.add_argument("--splits", default="1,2,4,8")
     ap.add_argument("--frame-batch", type=int, default=0,
-                    help="also time B frames per launch (RT_OPT_FRAME_BATCH) on one stream")
+                    help="also time B frames per launch (RT_OPT_FRAME_BATCH)")
+    ap.add_argument("--frame-streams", type=int, default=1,
+                    help="with --frame-batch: consecutive blocks of B frames go to S streams in "
+                         "turn (S launches of B frames in flight)")
     ap.add_argument("--layout", choices=("contiguous", "interleaved", "weighted"), default="contiguous",
                     help="weighted: contiguous bands cut by rt_weighted_band_rows over the "
                          "measured tile-row costs of one full-frame render (rt_tile_row_costs)")
@@ -116,7 +119,8 @@ def main():
     segs = torch.zeros(1, dtype=torch.int64, device=dev)
     n = args.launches
     res = {"config": args.config, "precision": args.precision, "width": W, "height": H,
-           "layout": args.layout, "splits": {}}
+           "layout": args.layout, "frame_batch": args.frame_batch, "frame_streams": args.frame_streams,
+           "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"), "splits": {}}
     inter = args.layout == "interleaved"
     weights = None
     if args.layout == "weighted":
@@ -168,23 +172,31 @@ def main():
             fbk = {}
             if args.frame_batch > 1:
                 B = args.frame_batch
+                S = max(1, min(4, args.frame_streams))
                 rend.set_option(capi.RT_OPT_FRAME_BATCH, B)
-                bufs = [out, out2] + [torch.empty((nr, W, 3), device=dev) for _ in range(B - 2)]
-                ptrs = [b_.data_ptr() for b_ in bufs[:B]]
+                bufs = [out, out2] + [torch.empty((nr, W, 3), device=dev) for _ in range(B * S - 2)]
+                ptrs = [b_.data_ptr() for b_ in bufs[:B * S]]
+                fst = ([st, st2] + list(extra))[:S]
+                sps = [s_.cuda_stream for s_ in fst for _ in range(B)]  # blocks of B frames per stream
                 for timed in (False, True):
                     torch.cuda.synchronize()
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record(st)
+                    for s_ in fst[1:]:
+                        s_.wait_stream(st)
                     rend.render_device_frames([cam], cfg.depth, ptrs, prec, row0=r0, nrows=nr,
-                                              streams=[st.cuda_stream], nframes=n if timed else 2 * B)
+                                              streams=sps, nframes=n if timed else 2 * B * S)
+                    for s_ in fst[1:]:
+                        st.wait_stream(s_)
                     e1.record(st)
                     torch.cuda.synchronize()
                 fbk[f"kernel_us_fb{B}"] = round(e0.elapsed_time(e1) / n * 1e3, 2)
-                with torch.cuda.stream(st):
-                    torch.cuda._sleep(int(2e8))
+                for s_ in fst:
+                    with torch.cuda.stream(s_):
+                        torch.cuda._sleep(int(2e8))
                 t0 = time.perf_counter()
                 rend.render_device_frames([cam], cfg.depth, ptrs, prec, row0=r0, nrows=nr,
-                                          streams=[st.cuda_stream], nframes=n)
+                                          streams=sps, nframes=n)
                 fbk[f"host_us_fb{B}"] = round((time.perf_counter() - t0) / n * 1e6, 2)
                 torch.cuda.synchronize()
                 rend.set_option(capi.RT_OPT_FRAME_BATCH, 1)
