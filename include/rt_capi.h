@@ -225,9 +225,11 @@ enum rt_option {
                                          RT_OPT_ROW_FEEDBACK, a change of the row order's
                                          grid, wave-cull scenes and RT_OPT_PIXEL_PAIRS launch
                                          one frame at a time.  On rt_multi_set_option: also
-                                         a rank renders its batch's bands (and the root its
-                                         rows) on one stream, so RT_OPT_MULTI_BATCH's band
-                                         frames become one launch.  Output is identical. */
+                                         a rank renders each RT_OPT_MULTI_BATCH batch's band
+                                         frames (and the root its rows) in blocks of B
+                                         consecutive frames per stream, over ceil(batch / B)
+                                         streams, so each block is one launch.  Output is
+                                         identical. */
     RT_OPT_MULTI_FRAMES = 17,        /* rt_multi_set_option only: F in [1, RT_MULTI_SLOTS]
                                          (default 2) band slots per rank — frames of a rank in
                                          flight on F render streams, so a small band's longest

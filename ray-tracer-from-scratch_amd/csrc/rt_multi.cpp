@@ -124,8 +124,8 @@ struct Rank {
     hipEvent_t ev_bdone[2] = {};
     // rt_multi_sync: recorded on each render stream and the comm stream, then polled
     hipEvent_t ev_drain[RT_MULTI_SLOTS + 1] = {};
-    // root, RT_OPT_FRAME_BATCH: its rows of a batch rendered (on the batch's first stream)
-    hipEvent_t ev_rows = nullptr;
+    // root, RT_OPT_FRAME_BATCH: its rows of a batch's block of frames rendered (per stream)
+    hipEvent_t ev_rows[RT_MULTI_SLOTS] = {};
     // worker thread (local ranks other than the first, one process driving several GPUs)
     std::thread th;
     std::mutex mu;
@@ -993,20 +993,21 @@ int batch_send(rt_multi* m, Rank* k, const BatchJob& b, bool self) {
     // the batch's frames round-robin over RT_OPT_MULTI_FRAMES render streams, so a small
     // band's long last waves overlap the next frames' (one stream would run them one after
     // another), each stream first waiting until this slot's last send is done
-    // (RT_OPT_FRAME_BATCH: every band frame on one stream, so the ctx launches the batch as
-    // one grid — its frames' tails overlap inside the launch)
-    const int S = m->frame_batch > 1 ? 1 : std::max(1, std::min(m->slots, b.kb));
-    void* sts[RT_MULTI_SLOTS];
-    for (int j = 0; j < S; j++) {
-        sts[j] = k->render_stream[j];
-        MHIPF(m, hipStreamWaitEvent(k->render_stream[j], k->ev_bsent[b.bs], 0));
-    }
+    // (RT_OPT_FRAME_BATCH = fb: blocks of fb consecutive frames per stream instead, over
+    // ceil(kb / fb) streams, so the ctx launches each block as one grid)
+    const int fb = m->frame_batch;
+    const int S = fb > 1 ? std::max(1, std::min(m->slots, (b.kb + fb - 1) / fb))
+                         : std::max(1, std::min(m->slots, b.kb));
+    for (int j = 0; j < S; j++) MHIPF(m, hipStreamWaitEvent(k->render_stream[j], k->ev_bsent[b.bs], 0));
+    void* sts[RT_MULTI_BATCH_MAX];  // frame i's stream
+    for (int i = 0; i < b.kb; i++)
+        sts[i] = k->render_stream[fb > 1 ? std::min(i / fb, S - 1) : i % S];
     void* outs[RT_MULTI_BATCH_MAX];
     for (int i = 0; i < b.kb; i++) outs[i] = static_cast<char*>(k->bbuf[b.bs]) + (size_t)i * bytes;
     {
         SlowCall sc_("rt_render_device_frames (batch)");
         const int e = rt_render_device_frames(k->ctx, b.cams, b.kb, pt.row0, pt.nrows, b.depth, b.precision,
-                                              b.flags, b.out_format, outs, b.kb, sts, S, b.kb);
+                                              b.flags, b.out_format, outs, b.kb, sts, b.kb, b.kb);
         if (e != RT_OK) return ctx_err(m, k, e, "rt_render_device_frames (batch)");
     }
     for (int j = 0; j < S; j++) {  // the send follows every stream's frames
@@ -1046,11 +1047,19 @@ int batch_root(rt_multi* m, Rank* k, const BatchJob& b, char* const* frames, hip
     // the next render into that buffer.  The previous batch's buffers wait on its done event;
     // the one before's on ev_bdone[bs], which still holds that batch's record (and the comm
     // stream runs batches in order, so it also covers every older one).
-    // RT_OPT_FRAME_BATCH: the root's rows of every frame of the batch are rendered on the
-    // first frame's stream (one launch); the batch's other caller streams are ordered around it
+    // RT_OPT_FRAME_BATCH = fb: the root's rows of each block of fb consecutive frames are
+    // rendered on the block's first frame's stream (one launch); a frame of another caller
+    // stream is ordered around it (its stream's earlier work before, its later work after)
+    const int fb = m->frame_batch;
     hipStream_t rs[RT_MULTI_BATCH_MAX];
-    for (int i = 0; i < b.kb; i++) rs[i] = m->frame_batch > 1 ? sts[0] : sts[i];
-    const bool one_stream = m->frame_batch > 1 && uniq.size() > 1;
+    bool cross = false;
+    for (int i = 0; i < b.kb; i++) {
+        rs[i] = fb > 1 ? sts[(i / fb) * fb] : sts[i];
+        cross = cross || rs[i] != sts[i];
+    }
+    std::vector<hipStream_t> rset;  // the streams that render
+    for (int i = 0; i < b.kb; i++)
+        if (std::find(rset.begin(), rset.end(), rs[i]) == rset.end()) rset.push_back(rs[i]);
     {
         std::vector<std::pair<hipStream_t, int>> waits;
         const int prev = 1 - b.bs;
@@ -1071,8 +1080,10 @@ int batch_root(rt_multi* m, Rank* k, const BatchJob& b, char* const* frames, hip
     for (size_t u = 0; u < uniq.size(); u++) {
         MHIPF(m, hipEventRecord(m->ev_in[u], uniq[u]));
         MHIPF(m, hipStreamWaitEvent(k->comm_stream, m->ev_in[u], 0));
-        // the root's rows of a frame of stream u, rendered on sts[0], follow u's earlier work
-        if (one_stream && uniq[u] != sts[0]) MHIPF(m, hipStreamWaitEvent(sts[0], m->ev_in[u], 0));
+        // the root's rows of a frame of stream u rendered on another stream follow u's earlier work
+        if (cross)
+            for (hipStream_t r : rset)
+                if (r != uniq[u]) MHIPF(m, hipStreamWaitEvent(r, m->ev_in[u], 0));
     }
     const Part p0 = part_of(m, cam.height, 0);
     int st = RT_OK;
@@ -1089,11 +1100,13 @@ int batch_root(rt_multi* m, Rank* k, const BatchJob& b, char* const* frames, hip
         const int e = rt_render_device_frames(k->ctx, b.cams, b.kb, p0.row0, p0.nrows, b.depth, b.precision,
                                               b.flags, b.out_format, outs, b.kb, ss, b.kb, b.kb);
         st = ctx_err(m, k, e, "rt_render_device_frames (root batch)");
-        if (st == RT_OK && one_stream) {
-            // work the caller enqueues on the batch's other streams sees their frames' rows
-            MHIPF(m, hipEventRecord(k->ev_rows, sts[0]));
-            for (hipStream_t u : uniq)
-                if (u != sts[0]) MHIPF(m, hipStreamWaitEvent(u, k->ev_rows, 0));
+        if (st == RT_OK && cross) {
+            // work the caller enqueues on the batch's streams sees their frames' rows
+            for (size_t j = 0; j < rset.size() && j < (size_t)RT_MULTI_SLOTS; j++) {
+                MHIPF(m, hipEventRecord(k->ev_rows[j], rset[j]));
+                for (hipStream_t u : uniq)
+                    if (u != rset[j]) MHIPF(m, hipStreamWaitEvent(u, k->ev_rows[j], 0));
+            }
         }
     }
     if (st != RT_OK) return st;
@@ -1230,7 +1243,8 @@ void destroy_rank(Rank* k, bool abort_comm) {
     }
     for (auto e : k->ev_drain)
         if (e) (void)hipEventDestroy(e);
-    if (k->ev_rows) (void)hipEventDestroy(k->ev_rows);
+    for (auto e : k->ev_rows)
+        if (e) (void)hipEventDestroy(e);
     for (auto& e : k->ev_ready)
         if (e) (void)hipEventDestroy(e);
     for (auto& b : k->staging)
@@ -1584,7 +1598,8 @@ int rt_multi_create(const int32_t* devices, int32_t nlocal, int32_t nranks, int3
         }
         for (auto& ev : k->ev_drain)
             if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&k->ev_rows, hipEventDisableTiming);
+        for (auto& ev : k->ev_rows)
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
         if (e != hipSuccess) fail(hip_err(m, e, "rank streams/events"));
     }
     if (st == RT_OK && m->has_root()) {

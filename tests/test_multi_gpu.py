@@ -412,7 +412,7 @@ def test_batched_gather_ragged_empty_bands_and_root_limits(rend, W, fmt):
 
 
 @pytest.mark.parametrize("transport,frame_batch", [("threads", 1), ("loopback", 1), ("threads", 4),
-                                                   ("loopback", 4)])
+                                                   ("loopback", 4), ("threads", 2), ("loopback", 2)])
 def test_batched_frames_each_whole_in_its_own_buffer(rend, transport, frame_batch):
     """B = 4 frames of a moving camera into 4 distinct buffers — every buffer
     bitwise against ITS OWN one-GPU frame (not only the last frame written) — then 4 more
@@ -422,7 +422,9 @@ def test_batched_frames_each_whole_in_its_own_buffer(rend, transport, frame_batc
     on the root before anything is enqueued; the one-rank handle stays usable, and with
     peers (THREADS) the exchange ends for every handle (RT_ERR_COMM, no hang).
     frame_batch 4 (RT_OPT_FRAME_BATCH): every rank's band frames of a batch, and the root's
-    rows of them over its two caller streams, go to the GPU as one launch."""
+    rows of them over its two caller streams, go to the GPU as one launch; frame_batch 2:
+    two launches of two frames on two streams per batch (the root's rows of a frame rendered
+    on the other caller stream's launch, ordered around it)."""
     import os
     import torch
     dev = torch.device("cuda", 0)
