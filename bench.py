@@ -271,14 +271,16 @@ def main(argv=None) -> int:
                          "(rt_weighted_band_rows, RT_OPT_MULTI_LAYOUT 2)")
     ap.add_argument("--rank-frames", type=int, default=4,
                     help="N > 1: band frames in flight per rank (RT_OPT_MULTI_FRAMES)")
-    ap.add_argument("--rank-batch", type=int, default=4,
+    ap.add_argument("--rank-batch", type=int, default=8,
                     help="N > 1: frames per gather (RT_OPT_MULTI_BATCH): each rank sends its bands "
                          "of that many frames in one ncclSend, the root scatters them with one "
                          "kernel (the per-frame exchange's host calls cost more than a 1/8 band)")
     ap.add_argument("--frame-batch", type=int, default=0,
-                    help="RT_OPT_FRAME_BATCH: a rank's band frames of one gather go to the GPU as "
-                         "one launch (0 = auto: the gather's batch at N > 1, else 1); at N = 1 an "
-                         "explicit B > 1 launches B consecutive frames of a stream as one grid")
+                    help="RT_OPT_FRAME_BATCH: frames per launch — at N > 1 a rank's band frames of "
+                         "one gather go to the GPU in blocks of this many per stream (0 = auto: 2, "
+                         "so a gather of 8 is 4 launches on 4 streams; tools/band_model.py, "
+                         "DESIGN §5); at N = 1 an explicit B > 1 launches B consecutive frames of "
+                         "a stream as one grid (measured slower than 2 streams: off)")
     ap.add_argument("--local-ranks", type=int, default=1,
                     help="rehearsal only (one process): split the frame over this many ranks "
                          "on this one GPU with the peer-copy transport; not a measurement")
@@ -405,8 +407,7 @@ def main(argv=None) -> int:
     torch.cuda.set_stream(stream)
     st_ptrs = [s_.cuda_stream for s_ in streams]
     rank_batch = max(1, min(capi.RT_MULTI_BATCH_MAX, args.rank_batch))
-    frame_batch = max(1, min(capi.RT_MULTI_BATCH_MAX,
-                             args.frame_batch if args.frame_batch > 0 else rank_batch))
+    frame_batch = max(1, min(capi.RT_MULTI_BATCH_MAX, args.frame_batch if args.frame_batch > 0 else 2))
     # frame buffers: the whole frame on rank 0 (tiled: the bands are gathered into it) or on
     # every rank (frames mode); fp32-RGB sized, which the sweep below also writes.  The
     # batched exchange (N > 1) needs a distinct buffer per frame of a batch (rt_capi.h
