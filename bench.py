@@ -566,10 +566,13 @@ def main(argv=None) -> int:
                       file=sys.stderr)
             del ref
 
-    if args.fault_rank == rank and multi is not None:
-        # test hook: this rank's next frame fails once its part of the exchange is queued
-        multi.set_option(capi.RT_OPT_MULTI_FAULT, 1)
-        print(f"bench rank {rank}: injecting a fault into the next frame", file=sys.stderr)
+    if args.fault_rank == rank:
+        if multi is not None:
+            # test hook: this rank's next frame fails once its part of the exchange is queued
+            multi.set_option(capi.RT_OPT_MULTI_FAULT, 1)
+            print(f"bench rank {rank}: injecting a fault into the next frame", file=sys.stderr)
+        else:   # the torch tiler: the rank fails outright (its peers wait in a collective)
+            raise RuntimeError(f"bench rank {rank}: injected failure (--fault-rank)")
 
     def run_steps(n: int):
         """n consecutive frames, enqueued by ONE C-ABI call (or the torch tiler's loop)."""

@@ -90,6 +90,19 @@ def test_self_launched_ipc_ranks_run_the_native_operator(n):
 
 @pytest.mark.gpu
 @pytest.mark.skipif(not has_gpu(), reason="needs a HIP device")
+def test_a_failed_rank_ends_the_gloo_rehearsal_nonzero():
+    """--fault-rank 1 on the gloo rehearsal (torch tiler): rank 1 fails after the gather
+    check while rank 0 waits in a collective; the supervisor stops rank 0 and exits
+    non-zero naming rank 1, well inside the deadline."""
+    p, dt = _bench(["--gpus", "2", "--fault-rank", "1"] + COMMON[:-2] + ["--deadline", "120"],
+                   env_extra={"RT_BENCH_BACKEND": "gloo"}, timeout=200)
+    assert p.returncode != 0
+    assert dt < 180
+    assert "bench supervisor: rank 1 exited" in p.stderr, p.stderr[-3000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not has_gpu(), reason="needs a HIP device")
 def test_a_failed_rank_ends_the_run_nonzero():
     """--fault-rank 1 (RT_OPT_MULTI_FAULT on rank 1, IPC transport): rank 1's frame fails
     after its send was queued; the run ends non-zero within the deadline, rank named."""
