@@ -1326,12 +1326,21 @@ int ipc_create(rt_multi* m, const uint8_t* id) {
     me.nranks = m->nranks;
     st_rel(&me.joined, 1u);
     x.joined = true;
+    int dead = -1;  // a rank that joined and whose process has exited since
     int st = ipc_wait(m, [&] {
-        for (int g = 0; g < m->nranks; g++)
-            if (!ld_acq(&x.sh->peer[g].joined)) return false;
-        return true;
+        bool all = true;
+        for (int g = 0; g < m->nranks; g++) {
+            const IpcPeer& pg = x.sh->peer[g];
+            if (!ld_acq(&pg.joined)) all = false;
+            else if (g != k->rank && dead < 0 && pid_gone(pg.pid)) dead = g;
+        }
+        return all || dead >= 0;
     }, -1, "IPC: waiting for every rank to join", std::max<int64_t>(hub_timeout_ms(), 120000));
     if (st != RT_OK) return st;
+    if (dead >= 0) {
+        std::snprintf(m->last_err, sizeof m->last_err, "IPC: rank %d's process exited while the ranks joined", dead);
+        return RT_ERR_COMM;
+    }
     for (int g = 0; g < m->nranks; g++)
         if (x.sh->peer[g].nranks != m->nranks) {
             std::snprintf(m->last_err, sizeof m->last_err, "IPC: rank %d has %d ranks, this rank %d", g,
