@@ -43,6 +43,8 @@ def _worker(rank, n, uid, case, q):
         w, h, nf, layout, batch, slots, weights, fault = (case[k] for k in (
             "w", "h", "nf", "layout", "batch", "slots", "weights", "fault"))
         fbatch = case.get("frame_batch", 1)
+        fmt = case.get("fmt", capi.RT_OUT_RGB_F32)
+        prec = case.get("prec", capi.RT_PREC_PATH64)
         prims = scenes.to_prims(scenes.CONFIGS["c2"].scene())
         cams = [_cam(w, h, 0.02 * k) for k in range(5)]
         m = capi.MultiRenderer([0], nranks=n, first_rank=rank, unique_id=uid,
@@ -58,11 +60,13 @@ def _worker(rank, n, uid, case, q):
                 m.set_row_weights(weights)
             nb = case["nb"]
             sts = [torch.cuda.Stream(dev) for _ in range(2)]
-            bufs = ([torch.full((h, w, 3), -1.0, device=dev) for _ in range(nb)] if rank == 0 else [])
+            nbytes = h * w * capi.load().rt_out_bytes_per_pixel(fmt)
+            bufs = ([torch.full((nbytes,), 255, dtype=torch.uint8, device=dev) for _ in range(nb)]
+                    if rank == 0 else [])
             torch.cuda.synchronize()
             if fault and rank == fault:
                 m.set_option(capi.RT_OPT_MULTI_FAULT, 1)
-            m.render_device_frames(cams, 4, [b.data_ptr() for b in bufs], capi.RT_PREC_PATH64,
+            m.render_device_frames(cams, 4, [b.data_ptr() for b in bufs], prec, 0, fmt,
                                    streams=[s.cuda_stream for s in (sts if rank == 0 else sts[:1])],
                                    nframes=nf)
             torch.cuda.synchronize()
@@ -107,31 +111,37 @@ def rend():
     r.close()
 
 
-@pytest.mark.parametrize("n,w,h,layout,batch,slots,fbatch", [
-    (2, 1920, 1080, 0, 1, 2, 1),    # config 4's frame, per-frame exchange, contiguous bands
-    (2, 1920, 1080, 2, 4, 4, 4),    # config 4's frame, the batched exchange bench.py times
-    (3, 480, 270, 1, 1, 2, 1),      # interleaved parts (staging + strided scatter)
-    (4, 640, 360, 2, 3, 3, 1),      # cost-weighted bands, batched (a third batch revisits buffers)
-    (4, 640, 360, 0, 3, 3, 3),      # the same with one launch per batch (RT_OPT_FRAME_BATCH)
-    (4, 203, 117, 0, 2, 2, 1),      # ragged bands, 1-byte-misaligned rows
+F32, RGBA8, F64 = 0, 2, 1   # rt_out_format: RT_OUT_RGB_F32, RT_OUT_RGBA8, RT_OUT_RGB_F64
+
+
+@pytest.mark.parametrize("n,w,h,layout,batch,slots,fbatch,fmt", [
+    (2, 1920, 1080, 0, 1, 2, 1, F32),    # config 4's frame, per-frame exchange, contiguous bands
+    (2, 1920, 1080, 2, 4, 4, 4, F32),    # config 4's frame, batched, one launch per batch
+    (4, 1920, 1080, 2, 8, 4, 2, RGBA8),  # config 4, the bench's N > 1 settings, RGBA8 transport
+    (3, 480, 270, 1, 1, 2, 1, F32),      # interleaved parts (staging + strided scatter)
+    (3, 480, 270, 1, 1, 2, 1, F64),      # the same, fp64 frames (F64 precision)
+    (4, 640, 360, 2, 3, 3, 1, F32),      # cost-weighted bands, batched (a third batch revisits buffers)
+    (4, 640, 360, 0, 3, 3, 3, F32),      # the same with one launch per batch (RT_OPT_FRAME_BATCH)
+    (4, 203, 117, 0, 2, 2, 1, RGBA8),    # ragged bands, RGBA8 rows of 812 B (4-byte scatter)
 ])
-def test_ipc_processes_gather_bitwise(rend, n, w, h, layout, batch, slots, fbatch):
+def test_ipc_processes_gather_bitwise(rend, n, w, h, layout, batch, slots, fbatch, fmt):
     from rtamd import capi, scenes
+    prec = capi.RT_PREC_F64 if fmt == F64 else capi.RT_PREC_PATH64
     prims = scenes.to_prims(scenes.CONFIGS["c2"].scene())
     rend.set_scene(prims)
     cams = [_cam(w, h, 0.02 * k) for k in range(5)]
-    refs = [rend.render(c, 4, capi.RT_PREC_PATH64, 0, capi.RT_OUT_RGB_F32)[0] for c in cams]
+    refs = [rend.render(c, 4, prec, 0, fmt)[0] for c in cams]
     weights = rend.tile_row_costs(cams[0], 4, capi.RT_PREC_PATH64).tolist() if layout == 2 else None
     nf = 7
     nb = 2 if batch == 1 else min(nf, 2 * batch)
     case = dict(w=w, h=h, nf=nf, layout=layout, batch=batch, slots=slots, weights=weights,
-                fault=0, nb=nb, frame_batch=fbatch)
+                fault=0, nb=nb, frame_batch=fbatch, fmt=fmt, prec=prec)
     res = _run(n, case)
     assert all(r["status"] == 0 for r in res), [(r["rank"], r["status"], r["error"]) for r in res]
     bufs = res[0]["bufs"]
     for b in range(nb):
         lf = max(f for f in range(nf) if f % nb == b)
-        assert np.array_equal(bufs[b].view(np.uint32), refs[lf % len(cams)].view(np.uint32)), (n, layout, b)
+        assert np.array_equal(bufs[b], refs[lf % len(cams)].view(np.uint8).reshape(-1)), (n, layout, fmt, b)
 
 
 @pytest.mark.parametrize("batch", [1, 4])
