@@ -68,7 +68,8 @@ PARITY = {  # what each precision guarantees vs the reference (tests/test_gpu_pa
     "f64": "per-pixel |delta| <= 1e-12 vs the reference's fp64 frames",
     "mixed": "bit-identical to f64",
     "path64": "exact fp64 ray paths (hits, normals, reflections); fp32 colour: every pixel "
-              "within 2e-5 of the reference, no discontinuity flips",
+              "within 2e-5 of the reference, no discontinuity flips (full c2 / c3 frames vs the "
+              "oracle: max |delta| 1.6e-6 / 2.0e-6, equal segment counts)",
     "f32": "|delta| <= 1e-4 on >= 99.5% of pixels at depth <= 4 (flips at discontinuities)",
 }
 
