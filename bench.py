@@ -164,13 +164,31 @@ def supervise(args, argv) -> int:
     port = free_port()
     script = os.path.abspath(__file__)
     procs, lines = [], []
+
+    def die_with_parent():
+        # a child gets SIGTERM if the supervisor dies (e.g. killed by an outer time limit)
+        import ctypes
+        try:
+            ctypes.CDLL(None, use_errno=True).prctl(1, signal.SIGTERM)   # PR_SET_PDEATHSIG
+        except (OSError, AttributeError):
+            pass
+
+    def on_term(signum, frame):
+        for p_ in procs:
+            if p_.poll() is None:
+                p_.send_signal(signal.SIGTERM)
+        print(f"bench supervisor: signal {signum}: ranks stopped", file=sys.stderr, flush=True)
+        os._exit(128 + signum)
+
+    signal.signal(signal.SIGTERM, on_term)
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
                    LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port))
         env.setdefault("GPU_MAX_HW_QUEUES", "16")
         procs.append(subprocess.Popen([sys.executable, "-u", script] + argv, env=env,
-                                      stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno()))
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno(),
+                                      preexec_fn=die_with_parent))
 
     def pump():
         for ln in procs[0].stdout:
@@ -325,6 +343,10 @@ def main(argv=None) -> int:
               file=sys.stderr)
         return 2
     start_watchdog(args.deadline, rank)
+    if os.environ.get("RT_BENCH_TEST_HANG"):   # test hook: a rank stuck before any GPU work
+        PHASE[0] = "test hang"
+        while True:
+            time.sleep(1)
 
     # stdout carries the ONE JSON line: anything the libraries print there (RCCL's version
     # banner when a communicator is made) goes to stderr, the JSON to a private copy of fd 1

@@ -48,6 +48,36 @@ def test_supervisor_reports_a_failed_rank_and_exits_nonzero():
     assert p.stdout.strip() == ""
 
 
+@pytest.mark.skipif(has_gpu(), reason="CPU-only: uses the supervisor without a GPU")
+@pytest.mark.parametrize("sig", ["SIGTERM", "SIGKILL"])
+def test_supervisor_stops_its_ranks_when_terminated(sig):
+    """SIGTERM or SIGKILL to the supervisor (an outer time limit) stops its rank processes
+    too: it forwards SIGTERM, and the ranks are tied to it (PR_SET_PDEATHSIG) for SIGKILL."""
+    import signal
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    # the children sleep in a stand-in for a hung rank: RT_BENCH_TEST_HANG makes main() wait
+    env["RT_BENCH_TEST_HANG"] = "1"
+    p = subprocess.Popen([sys.executable, BENCH, "--gpus", "2", "--deadline", "300"], env=env,
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, cwd=REPO,
+                         start_new_session=True)
+    time.sleep(8)
+    kids = [int(x) for x in subprocess.run(["pgrep", "-P", str(p.pid)], capture_output=True,
+                                           text=True).stdout.split()]
+    assert len(kids) == 2, kids
+    p.send_signal(getattr(signal, sig))
+    p.wait(timeout=30)
+    assert p.returncode != 0
+    t0 = time.monotonic()
+    while time.monotonic() - t0 < 20 and any(os.path.exists(f"/proc/{k}") and
+                                             open(f"/proc/{k}/stat").read().split()[2] != "Z"
+                                             for k in kids):
+        time.sleep(0.2)
+    assert not any(os.path.exists(f"/proc/{k}") and open(f"/proc/{k}/stat").read().split()[2] != "Z"
+                   for k in kids), kids
+
+
 def test_world_size_that_disagrees_with_gpus_is_an_error():
     p, _ = _bench(["--gpus", "2"], env_extra={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"},
                   timeout=120)
