@@ -35,7 +35,7 @@ Process model: one process per GPU.  Under a launcher (torch.distributed.run: RA
 WORLD_SIZE / LOCAL_RANK / MASTER_* in the environment) every process is one rank.  Without
 one, `--gpus N` > 1 makes this process a supervisor: it starts N child processes of this
 script (one per rank, RANK = LOCAL_RANK = r, MASTER_ADDR 127.0.0.1, a free port,
-GPU_MAX_HW_QUEUES=16) before anything touches the GPU, forwards rank 0's JSON line, and if
+GPU_MAX_HW_QUEUES = --hw-queues) before anything touches the GPU, forwards rank 0's JSON line, and if
 any child exits non-zero or the --deadline passes it stops the others and exits non-zero
 naming the rank.  Every rank also has its own deadline watchdog.  `--transport ipc` runs
 the row-tiled operator's process-per-GPU code across processes on ONE GPU
@@ -50,12 +50,6 @@ import sys
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
-# N > 1: every rank keeps RT_OPT_MULTI_FRAMES (4) band frames in flight on their own streams,
-# which need their own hardware queues (HIP's default is 4 per process, shared round-robin by
-# every stream the process makes: with it 4 band frames in flight were no faster than 2 —
-# tools/band_model.py).  Read by the HIP runtime at its initialisation.
-if int(os.environ.get("WORLD_SIZE", "1")) > 1:
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
 sys.path.insert(0, os.path.join(REPO, "ray-tracer-from-scratch_amd"))
 
 from rtamd import capi, scenes  # noqa: E402
@@ -185,7 +179,8 @@ def supervise(args, argv) -> int:
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
                    LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port))
-        env.setdefault("GPU_MAX_HW_QUEUES", "16")
+        if args.hw_queues > 0:
+            env["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
         procs.append(subprocess.Popen([sys.executable, "-u", script] + argv, env=env,
                                       stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno(),
                                       preexec_fn=die_with_parent))
@@ -323,6 +318,13 @@ def main(argv=None) -> int:
     ap.add_argument("--box-cache", type=int, default=0, choices=[0, 1],
                     help="RT_OPT_BOX_CACHE: reuse the host's per-frame pixel boxes when the "
                          "camera is unchanged (0 = recompute every frame)")
+    ap.add_argument("--hw-queues", type=int, default=16, choices=range(0, 33), metavar="Q",
+                    help="N > 1: GPU_MAX_HW_QUEUES for each rank (0 = leave the environment's). "
+                         "A rank keeps RT_OPT_MULTI_FRAMES band frames in flight on their own "
+                         "streams, which need their own hardware queues: HIP's default (and the "
+                         "GPU boxes' environment) is 4 per process, shared round-robin by every "
+                         "stream it makes (tools/band_model.py, DESIGN §5).  Set before HIP "
+                         "initialises, so it overrides the environment's value")
     ap.add_argument("--deadline", type=float, default=900.0,
                     help="seconds: the supervisor (and each rank's watchdog) ends the run "
                          "non-zero if it is still going")
@@ -343,6 +345,8 @@ def main(argv=None) -> int:
               file=sys.stderr)
         return 2
     start_watchdog(args.deadline, rank)
+    if world > 1 and args.hw_queues > 0:   # read by the HIP runtime at its initialisation
+        os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
     if os.environ.get("RT_BENCH_TEST_HANG"):   # test hook: a rank stuck before any GPU work
         PHASE[0] = "test hang"
         while True:
