@@ -34,8 +34,8 @@ kernel time; the frame-sharded side run (N > 1); the CPU baseline (rank 0, N = 1
 Process model: one process per GPU.  Under a launcher (torch.distributed.run: RANK /
 WORLD_SIZE / LOCAL_RANK / MASTER_* in the environment) every process is one rank.  Without
 one, `--gpus N` > 1 makes this process a supervisor: it starts N child processes of this
-script (one per rank, RANK = LOCAL_RANK = r, MASTER_ADDR 127.0.0.1, a free port,
-GPU_MAX_HW_QUEUES = --hw-queues) before anything touches the GPU, forwards rank 0's JSON line, and if
+script (one per rank, RANK = LOCAL_RANK = r, MASTER_ADDR 127.0.0.1, a free port) before
+anything touches the GPU, forwards rank 0's JSON line, and if
 any child exits non-zero or the --deadline passes it stops the others and exits non-zero
 naming the rank.  Every rank also has its own deadline watchdog.  `--transport ipc` runs
 the row-tiled operator's process-per-GPU code across processes on ONE GPU
@@ -179,8 +179,6 @@ def supervise(args, argv) -> int:
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
                    LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port))
-        if args.hw_queues > 0:
-            env["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
         procs.append(subprocess.Popen([sys.executable, "-u", script] + argv, env=env,
                                       stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno(),
                                       preexec_fn=die_with_parent))
@@ -319,12 +317,15 @@ def main(argv=None) -> int:
                     help="RT_OPT_BOX_CACHE: reuse the host's per-frame pixel boxes when the "
                          "camera is unchanged (0 = recompute every frame)")
     ap.add_argument("--hw-queues", type=int, default=16, choices=range(0, 33), metavar="Q",
-                    help="N > 1: GPU_MAX_HW_QUEUES for each rank (0 = leave the environment's). "
-                         "A rank keeps RT_OPT_MULTI_FRAMES band frames in flight on their own "
-                         "streams, which need their own hardware queues: HIP's default (and the "
-                         "GPU boxes' environment) is 4 per process, shared round-robin by every "
-                         "stream it makes (tools/band_model.py, DESIGN §5).  Set before HIP "
-                         "initialises, so it overrides the environment's value")
+                    help="N > 1 with a GPU per rank: GPU_MAX_HW_QUEUES for each rank (0 = leave "
+                         "the environment's).  A rank keeps RT_OPT_MULTI_FRAMES band frames in "
+                         "flight on their own streams, which need their own hardware queues: "
+                         "HIP's default (and the GPU boxes' environment) is 4 per process, shared "
+                         "round-robin by every stream it makes (tools/band_model.py, DESIGN §5).  "
+                         "Set before HIP initialises, so it overrides the environment's value.  "
+                         "Ranks that share a GPU (rehearsals) keep the environment's: several "
+                         "processes with 16 queues each on one GPU run far slower "
+                         "(tools/ab_hw_queues.sh, profiles/r06/probes/ab_hw_queues.jsonl)")
     ap.add_argument("--deadline", type=float, default=900.0,
                     help="seconds: the supervisor (and each rank's watchdog) ends the run "
                          "non-zero if it is still going")
@@ -345,8 +346,6 @@ def main(argv=None) -> int:
               file=sys.stderr)
         return 2
     start_watchdog(args.deadline, rank)
-    if world > 1 and args.hw_queues > 0:   # read by the HIP runtime at its initialisation
-        os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
     if os.environ.get("RT_BENCH_TEST_HANG"):   # test hook: a rank stuck before any GPU work
         PHASE[0] = "test hang"
         while True:
@@ -360,6 +359,11 @@ def main(argv=None) -> int:
 
     import torch
     import torch.distributed as dist
+
+    # read by the HIP runtime at its initialisation (below: torch.cuda.set_device); counting
+    # devices does not initialise it on this image
+    if world > 1 and args.hw_queues > 0 and world <= torch.cuda.device_count():
+        os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
 
     # RT_BENCH_BACKEND=gloo (or --transport ipc): rehearsal of the N-rank code path on fewer
     # GPUs than ranks (ranks share devices round-robin; RCCL refuses two ranks on one GPU, so

@@ -116,8 +116,9 @@ def test_self_launched_ipc_ranks_run_the_native_operator(n):
     assert g["batched"]["every_buffer_bitwise_equal"] and g["per_frame"]["every_buffer_bitwise_equal"], g
     assert "HIP IPC" in g["operator"]
     assert r["config"]["band_layout"] == "weighted"
-    # --hw-queues (16) overrides the box's GPU_MAX_HW_QUEUES=4 in every rank
-    assert r["config"]["gpu_max_hw_queues"] == "16"
+    # ranks sharing one GPU keep the environment's hardware queues (--hw-queues applies with a
+    # GPU per rank: several processes with 16 queues each on one GPU run far slower)
+    assert r["config"]["gpu_max_hw_queues"] == os.environ.get("GPU_MAX_HW_QUEUES")
 
 
 @pytest.mark.gpu
